@@ -1,0 +1,177 @@
+"""ctypes binding of libactalker_hip.so (the C ABI declared in include/actalker_hip.h).
+
+The shared library is built in-tree by ``actalker_amd/csrc/Makefile`` (``__graft_entry__.build``).
+There is deliberately no fallback: if the library cannot be loaded every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libactalker_hip.so")
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_ll = ctypes.c_longlong
+c_vp = ctypes.c_void_p
+c_fp = ctypes.POINTER(ctypes.c_float)
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("A", c_vp), ("A2", c_vp), ("lda", c_int), ("lda2", c_int), ("K1", c_int),
+        ("amode", c_int),
+        ("H", c_int), ("W", c_int), ("Ho", c_int), ("Wo", c_int), ("conv_stride", c_int), ("upsample", c_int),
+        ("Cin", c_int),
+        ("F", c_int), ("S", c_int),
+        ("B", c_vp), ("ldb", c_int),
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("bias", c_vp),
+        ("rowbias", c_vp), ("rb_div", c_int), ("ldrb", c_int),
+        ("R", c_vp), ("ldr", c_int), ("rmap", c_vp), ("r_div", c_int), ("r_mod", c_int),
+        ("MIX", c_vp), ("ldmix", c_int), ("mix_alpha", c_float),
+        ("alpha", c_float),
+        ("act", c_int),
+        ("out_f32", c_int),
+        ("C", c_vp), ("ldc", c_int),
+        ("orow_div", c_int), ("orow_stride", c_int), ("orow_off", c_int),
+    ]
+
+
+class AttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("q", c_vp), ("k", c_vp), ("v", c_vp), ("o", c_vp),
+        ("ldq", c_int), ("ldk", c_int), ("ldv", c_int), ("ldo", c_int),
+        ("bsq", c_ll), ("bsk", c_ll), ("bsv", c_ll), ("bso", c_ll),
+        ("nbatch", c_int), ("nheads", c_int), ("Sq", c_int), ("Skv", c_int),
+        ("scale", c_float),
+    ]
+
+
+class TemporalAttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("qkv", c_vp), ("ldqkv", c_int), ("o", c_vp), ("ldo", c_int),
+        ("B", c_int), ("F", c_int), ("S", c_int), ("H", c_int),
+        ("scale", c_float),
+    ]
+
+
+class IpAttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("q", c_vp), ("ldq", c_int),
+        ("kv", c_vp), ("ldkv", c_int), ("nkeys", c_int),
+        ("vbase", c_vp), ("ldvbase", c_int),
+        ("vb", c_vp), ("ldvb", c_int),
+        ("mask_a", c_vp), ("mask_b", c_vp),
+        ("sa", c_float), ("sb", c_float), ("scale", c_float),
+        ("out", c_vp), ("ldo", c_int),
+        ("M", c_int), ("H", c_int), ("rows_per_ctx", c_int), ("S", c_int),
+    ]
+
+
+class LayerNormDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_int),
+        ("add", c_vp), ("ldadd", c_int), ("add_div", c_int),
+        ("sum_out", c_vp), ("ldsum", c_int),
+        ("gamma", c_vp), ("beta", c_vp), ("eps", c_float),
+        ("y", c_vp), ("ldy", c_int),
+        ("M", c_int), ("C", c_int),
+    ]
+
+
+class GroupNormDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_int), ("x2", c_vp), ("ldx2", c_int), ("C1", c_int),
+        ("M", c_int), ("C", c_int), ("G", c_int), ("rows_per_stat", c_int),
+        ("gamma", c_vp), ("beta", c_vp), ("eps", c_float),
+        ("silu", c_int),
+        ("y", c_vp), ("ldy", c_int),
+        ("ws", c_vp),
+    ]
+
+
+class MambaCombineDesc(ctypes.Structure):
+    _fields_ = [
+        ("xa", c_vp), ("ldxa", c_int), ("ya0", c_vp), ("ya1", c_vp), ("ldya", c_int), ("La", c_int),
+        ("pos_a", c_vp), ("mode_a", c_int),
+        ("xe", c_vp), ("ldxe", c_int), ("ye0", c_vp), ("ye1", c_vp), ("ldye", c_int), ("Le", c_int),
+        ("pos_e", c_vp), ("mode_e", c_int),
+        ("gamma", c_vp), ("beta", c_vp), ("eps", c_float),
+        ("y", c_vp), ("ldy", c_int),
+        ("M", c_int), ("S", c_int), ("C", c_int),
+    ]
+
+
+class ScanDesc(ctypes.Structure):
+    _fields_ = [
+        ("u", c_vp), ("ldu", c_int),
+        ("xdbl", c_vp), ("ldx", c_int),
+        ("dt_w", c_vp), ("dt_b", c_vp), ("A_log", c_vp), ("Dskip", c_vp),
+        ("y0", c_vp), ("y1", c_vp), ("ldy", c_int),
+        ("nb", c_int), ("L", c_int), ("D", c_int), ("R", c_int), ("N", c_int), ("n_keep", c_int),
+        ("delta", c_vp), ("ld_delta", c_int), ("delta_f32", c_int), ("softplus", c_int),
+        ("G", c_int), ("u_gstride", c_int), ("y_gstride", c_int), ("flip1", c_int),
+    ]
+
+
+# Every symbol include/actalker_hip.h declares, with its ctypes signature.
+_P = ctypes.POINTER
+SIGNATURES = {
+    "acth_gemm": ([_P(GemmDesc), c_vp], c_int),
+    "acth_gemm_desc_size": ([], c_int),
+    "acth_flash_attn": ([_P(AttnDesc), c_vp], c_int),
+    "acth_temporal_attn": ([_P(TemporalAttnDesc), c_vp], c_int),
+    "acth_ip_attn": ([_P(IpAttnDesc), c_vp], c_int),
+    "acth_layernorm": ([_P(LayerNormDesc), c_vp], c_int),
+    "acth_groupnorm": ([_P(GroupNormDesc), c_vp], c_int),
+    "acth_groupnorm_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
+    "acth_mamba_combine_ln": ([_P(MambaCombineDesc), c_vp], c_int),
+    "acth_selective_scan": ([_P(ScanDesc), c_vp], c_int),
+    "acth_timestep_embedding": ([c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_vp, c_vp], c_int),
+    "acth_nchw_to_tokens": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "acth_tokens_to_nchw": ([c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "acth_im2col3x3": ([c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp], c_int),
+    "acth_gather_rows": ([c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
+    "acth_frame_mean": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp], c_int),
+    "acth_window_input": ([c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_int, c_vp], c_int),
+    "acth_cfg_euler_accum": ([c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp, c_vp,
+                              c_int, c_int, c_vp], c_int),
+    "acth_div_counter": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
+    "acth_version": ([], c_int),
+}
+
+_lib = None
+
+
+class ActhError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (once). Raises if it is missing: there is no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ActhError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C actalker_amd/csrc`). The ACTalker MI355X path has no fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (argtypes, restype) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    if lib.acth_gemm_desc_size() != ctypes.sizeof(GemmDesc):
+        raise ActhError("ActhGemmDesc layout mismatch between include/actalker_hip.h and _lib.py")
+    _lib = lib
+    return lib
+
+
+_ERR = {-1: "invalid argument (shape/alignment rejected)", -2: "kernel launch failed"}
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise ActhError(f"{what}: {_ERR.get(rc, rc)}")

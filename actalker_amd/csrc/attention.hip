@@ -1,0 +1,365 @@
+// Attention kernels for the SVD spatio-temporal UNet (head_dim = 64 everywhere).
+//
+//  * acth_flash_attn   : spatial self-attention softmax(Q K^T * scale) V over S <= 9216 tokens
+//                        (AttnProcessor2_0, reference attention_processor.py:1528-1605).
+//                        Flash-style online softmax on v_mfma_f32_32x32x16_bf16. The QK^T
+//                        product is computed transposed (S^T = K Q^T) so each lane owns one
+//                        query column: row max / row sum stay lane-local (+1 lane^32 exchange),
+//                        and S^T's accumulator registers feed the P.V product directly as the
+//                        B operand (O^T = V^T P^T), so no LDS round trip for P.
+//  * acth_temporal_attn: self-attention over the F (<=16) frames of a window at every spatial
+//                        position (TemporalBasicTransformerBlock.attn1, attention.py:446-448).
+//  * acth_ip_attn      : IP-adapter cross attention (IPAdapterAttnProcessor2_0,
+//                        attention_processor.py:2747-2934). 1-key attentions (ID, VASA) are
+//                        exactly their V row (softmax over one key == 1), so only the 32-key
+//                        audio attention is evaluated; region masks weight it per token.
+#include "common.h"
+
+// ------------------------------------------------------------------------------------------
+
+#define FA_LDS 72
+
+__global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 64 * FA_LDS];
+  bf16_t* Ks = smem;                 // [64 keys][72]   rows = key, cols = d
+  bf16_t* Vt = smem + 64 * FA_LDS;   // [64 d][72]      rows = d, cols = key
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y, bat = blockIdx.z;
+  const int q = blockIdx.x * 128 + wave * 32 + r32;
+  const bf16_t* qb = (const bf16_t*)p.q + bat * p.bsq + h * 64;
+  const bf16_t* kb = (const bf16_t*)p.k + bat * p.bsk + h * 64;
+  const bf16_t* vb = (const bf16_t*)p.v + bat * p.bsv + h * 64;
+
+  // Q^T fragments as the B operand: lane holds Q[q][16s + 8hh + j]
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint4 t = make_uint4(0, 0, 0, 0);
+    if (q < p.Sq) t = *reinterpret_cast<const uint4*>(qb + (size_t)q * p.ldq + 16 * s + 8 * hh);
+    qf[s] = *reinterpret_cast<bf16x8_t*>(&t);
+  }
+
+  const float c = p.scale * 1.4426950408889634f;   // fold log2(e): p = exp2(s*c - m)
+  float m_run = -INFINITY, l_run = 0.0f;
+  f32x16_t o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
+
+  for (int kv0 = 0; kv0 < p.Skv; kv0 += 64) {
+    // ---- stage K (row-major) and V^T into LDS ----
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cidx = tid + 256 * i;
+      // K: chunk-fastest mapping (coalesced rows)
+      {
+        const int row = cidx >> 3, kc = cidx & 7;
+        uint4 t = make_uint4(0, 0, 0, 0);
+        if (kv0 + row < p.Skv) t = *reinterpret_cast<const uint4*>(kb + (size_t)(kv0 + row) * p.ldk + kc * 8);
+        *reinterpret_cast<uint4*>(&Ks[row * FA_LDS + kc * 8]) = t;
+      }
+      // V: key-fastest mapping so the transposed 2-byte stores are bank-conflict free
+      {
+        const int row = cidx & 63, kc = cidx >> 6;
+        uint4 t = make_uint4(0, 0, 0, 0);
+        if (kv0 + row < p.Skv) t = *reinterpret_cast<const uint4*>(vb + (size_t)(kv0 + row) * p.ldv + kc * 8);
+        const bf16_t* e = reinterpret_cast<const bf16_t*>(&t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Vt[(kc * 8 + j) * FA_LDS + row] = e[j];
+      }
+    }
+    __syncthreads();
+
+    // ---- S^T = K Q^T for two 32-key subtiles ----
+    f32x16_t st[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[sub][r] = 0.0f;
+      const bf16_t* kr = Ks + (sub * 32 + r32) * FA_LDS + 8 * hh;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kr + 16 * s);
+        st[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], st[sub], 0, 0, 0);
+      }
+    }
+    // ---- online softmax (lane = query column) ----
+    float mx = -INFINITY;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        float sv = st[sub][r] * c;
+        if (key >= p.Skv) sv = -INFINITY;
+        st[sub][r] = sv;
+        mx = fmaxf(mx, sv);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    l_run *= alpha;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p0 = exp2f(st[sub][8 * s2 + 2 * j] - m_new);
+          const float p1 = exp2f(st[sub][8 * s2 + 2 * j + 1] - m_new);
+          l_run += p0 + p1;
+          w[j] = pack2(p0, p1);
+        }
+        pf[sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
+      }
+    // ---- O^T += V^T P^T ----
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kbase = sub * 32 + 16 * s2 + 4 * hh;
+        uint2 lo0 = *reinterpret_cast<const uint2*>(&Vt[r32 * FA_LDS + kbase]);
+        uint2 hi0 = *reinterpret_cast<const uint2*>(&Vt[r32 * FA_LDS + kbase + 8]);
+        uint2 lo1 = *reinterpret_cast<const uint2*>(&Vt[(32 + r32) * FA_LDS + kbase]);
+        uint2 hi1 = *reinterpret_cast<const uint2*>(&Vt[(32 + r32) * FA_LDS + kbase + 8]);
+        uint4 a0 = make_uint4(lo0.x, lo0.y, hi0.x, hi0.y);
+        uint4 a1 = make_uint4(lo1.x, lo1.y, hi1.x, hi1.y);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8_t*>(&a0), pf[sub][s2], o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8_t*>(&a1), pf[sub][s2], o1, 0, 0, 0);
+      }
+    __syncthreads();
+  }
+
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (q >= p.Sq) return;
+  const float inv = 1.0f / l_run;
+  bf16_t* ob = (bf16_t*)p.o + bat * p.bso + (size_t)q * p.ldo + h * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d0 = 8 * g + 4 * hh;
+    uint2 w0, w1;
+    w0.x = pack2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
+    w0.y = pack2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+    w1.x = pack2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
+    w1.y = pack2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    *reinterpret_cast<uint2*>(ob + d0) = w0;
+    *reinterpret_cast<uint2*>(ob + 32 + d0) = w1;
+  }
+}
+
+extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
+  if (!d || !d->q || !d->k || !d->v || !d->o) return ACTH_EINVAL;
+  if (d->Sq <= 0 || d->Skv <= 0 || d->nheads <= 0 || d->nbatch <= 0) return ACTH_EINVAL;
+  if (d->ldq % 8 || d->ldk % 8 || d->ldv % 8 || d->ldo % 4) return ACTH_EINVAL;
+  if (d->nheads > 65535 || d->nbatch > 65535) return ACTH_EINVAL;
+  dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
+  hipLaunchKernelGGL(flash_attn_kernel, grid, dim3(256), 0, stream, *d);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Temporal self-attention over frames. qkv rows are tokens (b, f, s) = (b*F + f)*S + s with
+// [q | k | v] column blocks of width C = H*64. Output o rows use the same token order.
+
+#define TA_TUPLES 16
+
+__global__ __launch_bounds__(256) void temporal_attn_kernel(const ActhTemporalAttnDesc p) {
+  __shared__ __attribute__((aligned(16))) bf16_t sk[TA_TUPLES][16][64];
+  __shared__ __attribute__((aligned(16))) bf16_t sv[TA_TUPLES][16][64];
+  const int tid = threadIdx.x;
+  const long long ntup = (long long)p.B * p.S * p.H;
+  const long long tup0 = (long long)blockIdx.x * TA_TUPLES;
+  const int C = p.H * 64;
+
+  // stage K and V rows: tuple tl, frame f, chunk kc
+  for (int idx = tid; idx < TA_TUPLES * 16 * 8; idx += 256) {
+    const int kc = idx & 7, f = (idx >> 3) & 15, tl = idx >> 7;
+    const long long tp = tup0 + tl;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (tp < ntup && f < p.F) {
+      const int h = (int)(tp % p.H);
+      const long long bs = tp / p.H;
+      const int s = (int)(bs % p.S), b = (int)(bs / p.S);
+      const size_t row = ((size_t)b * p.F + f) * p.S + s;
+      const bf16_t* base = (const bf16_t*)p.qkv + row * p.ldqkv + h * 64 + kc * 8;
+      kv = *reinterpret_cast<const uint4*>(base + C);
+      vv = *reinterpret_cast<const uint4*>(base + 2 * C);
+    }
+    *reinterpret_cast<uint4*>(&sk[tl][f][kc * 8]) = kv;
+    *reinterpret_cast<uint4*>(&sv[tl][f][kc * 8]) = vv;
+  }
+  __syncthreads();
+
+  const int tl = tid >> 4, fq = tid & 15;
+  const long long tp = tup0 + tl;
+  if (tp >= ntup || fq >= p.F) return;
+  const int h = (int)(tp % p.H);
+  const long long bs = tp / p.H;
+  const int s = (int)(bs % p.S), b = (int)(bs / p.S);
+  const size_t row = ((size_t)b * p.F + fq) * p.S + s;
+
+  float qv[64];
+  const bf16_t* qrow = (const bf16_t*)p.qkv + row * p.ldqkv + h * 64;
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc) unpack8(*reinterpret_cast<const uint4*>(qrow + cc * 8), qv + cc * 8);
+
+  float sc[16];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int fk = 0; fk < 16; ++fk) {
+    float acc = 0.0f;
+    if (fk < p.F) {
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) {
+        float kf[8];
+        unpack8(*reinterpret_cast<const uint4*>(&sk[tl][fk][cc * 8]), kf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc = fmaf(qv[cc * 8 + e], kf[e], acc);
+      }
+      acc *= p.scale;
+      mx = fmaxf(mx, acc);
+    }
+    sc[fk] = acc;
+  }
+  float den = 0.0f;
+#pragma unroll
+  for (int fk = 0; fk < 16; ++fk) {
+    const float e = fk < p.F ? __expf(sc[fk] - mx) : 0.0f;
+    sc[fk] = e;
+    den += e;
+  }
+  const float inv = 1.0f / den;
+  float ov[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) ov[d] = 0.0f;
+#pragma unroll
+  for (int fk = 0; fk < 16; ++fk) {
+    if (fk < p.F) {
+      const float w = sc[fk] * inv;
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) {
+        float vf[8];
+        unpack8(*reinterpret_cast<const uint4*>(&sv[tl][fk][cc * 8]), vf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[cc * 8 + e] = fmaf(w, vf[e], ov[cc * 8 + e]);
+      }
+    }
+  }
+  bf16_t* orow = (bf16_t*)p.o + row * p.ldo + h * 64;
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc) *reinterpret_cast<uint4*>(orow + cc * 8) = pack8(ov + cc * 8);
+}
+
+extern "C" int acth_temporal_attn(const ActhTemporalAttnDesc* d, hipStream_t stream) {
+  if (!d || !d->qkv || !d->o) return ACTH_EINVAL;
+  if (d->F <= 0 || d->F > 16 || d->B <= 0 || d->S <= 0 || d->H <= 0) return ACTH_EINVAL;
+  if (d->ldqkv % 8 || d->ldo % 8) return ACTH_EINVAL;
+  const long long ntup = (long long)d->B * d->S * d->H;
+  const long long nblk = (ntup + TA_TUPLES - 1) / TA_TUPLES;
+  if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
+  hipLaunchKernelGGL(temporal_attn_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// IP-adapter cross attention, combined pre-projection output:
+//   out[m, :] = vbase[ctx, :] + sa * ma[s] * softmax(q_h K_h^T * scale) V_h  (32-key audio tokens)
+//             + sb * mb[s] * vb[ctx, :]                                     (1-key VASA token)
+// ctx = m / rows_per_ctx (frame for spatial blocks, batch for temporal blocks), s = m % S.
+// kv rows: ctx*nkeys + key, K in columns [0, C), V in [C, 2C).
+
+__global__ __launch_bounds__(256) void ip_attn_kernel(const ActhIpAttnDesc p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = blockIdx.y * 4 + wave;
+  const long long m = (long long)blockIdx.x * 64 + lane;
+  if (h >= p.H || m >= p.M) return;
+  const int C = p.H * 64;
+  const long long ctx = m / p.rows_per_ctx;
+  const int s = (int)(m % p.S);
+
+  float acc[64];
+  {
+    const bf16_t* vrow = (const bf16_t*)p.vbase + ctx * p.ldvbase + h * 64;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) unpack8(*reinterpret_cast<const uint4*>(vrow + cc * 8), acc + cc * 8);
+  }
+  if (p.vb) {
+    const float w = p.sb * (p.mask_b ? p.mask_b[s] : 1.0f);
+    const bf16_t* vrow = (const bf16_t*)p.vb + ctx * p.ldvb + h * 64;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) {
+      float t[8];
+      unpack8(*reinterpret_cast<const uint4*>(vrow + cc * 8), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[cc * 8 + e] = fmaf(w, t[e], acc[cc * 8 + e]);
+    }
+  }
+  if (p.kv) {
+    float qv[64];
+    const bf16_t* qrow = (const bf16_t*)p.q + m * p.ldq + h * 64;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) unpack8(*reinterpret_cast<const uint4*>(qrow + cc * 8), qv + cc * 8);
+    const bf16_t* kbase = (const bf16_t*)p.kv + ctx * p.nkeys * (long long)p.ldkv + h * 64;
+    float sc[32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      float a = -INFINITY;
+      if (j < p.nkeys) {
+        a = 0.0f;
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          float kf[8];
+          unpack8(*reinterpret_cast<const uint4*>(kbase + (size_t)j * p.ldkv + cc * 8), kf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a = fmaf(qv[cc * 8 + e], kf[e], a);
+        }
+        a *= p.scale;
+      }
+      sc[j] = a;
+      mx = fmaxf(mx, a);
+    }
+    float den = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) { const float e = j < p.nkeys ? __expf(sc[j] - mx) : 0.0f; sc[j] = e; den += e; }
+    const float w0 = p.sa * (p.mask_a ? p.mask_a[s] : 1.0f) / den;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      if (j < p.nkeys) {
+        const float w = w0 * sc[j];
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          float vf[8];
+          unpack8(*reinterpret_cast<const uint4*>(kbase + (size_t)j * p.ldkv + C + cc * 8), vf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[cc * 8 + e] = fmaf(w, vf[e], acc[cc * 8 + e]);
+        }
+      }
+    }
+  }
+  bf16_t* orow = (bf16_t*)p.out + m * p.ldo + h * 64;
+#pragma unroll
+  for (int cc = 0; cc < 8; ++cc) *reinterpret_cast<uint4*>(orow + cc * 8) = pack8(acc + cc * 8);
+}
+
+extern "C" int acth_ip_attn(const ActhIpAttnDesc* d, hipStream_t stream) {
+  if (!d || !d->vbase || !d->out) return ACTH_EINVAL;
+  if (d->kv && (!d->q || d->nkeys <= 0 || d->nkeys > 32 || d->ldkv % 8 || d->ldq % 8)) return ACTH_EINVAL;
+  if (d->M <= 0 || d->H <= 0 || d->rows_per_ctx <= 0 || d->S <= 0) return ACTH_EINVAL;
+  if (d->ldvbase % 8 || d->ldo % 8 || (d->vb && d->ldvb % 8)) return ACTH_EINVAL;
+  const long long nblk = ((long long)d->M + 63) / 64;
+  if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
+  dim3 grid((unsigned)nblk, (d->H + 3) / 4);
+  hipLaunchKernelGGL(ip_attn_kernel, grid, dim3(256), 0, stream, *d);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}

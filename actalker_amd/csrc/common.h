@@ -1,0 +1,66 @@
+// Shared device helpers for the ACTalker denoising-path kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include "../../include/actalker_hip.h"
+
+typedef uint16_t bf16_t;                                          // raw bf16 bits in HBM
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));      // MFMA A/B fragment
+typedef float f32x16_t __attribute__((ext_vector_type(16)));      // 32x32 MFMA accumulator
+typedef float f32x4_t __attribute__((ext_vector_type(4)));        // 16x16 MFMA accumulator
+
+#define ACTH_CHECK_LAUNCH()                                  \
+  do {                                                       \
+    if (hipGetLastError() != hipSuccess) return ACTH_ELAUNCH; \
+  } while (0)
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  // lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+  return __bfloat16_as_ushort(__float2bfloat16(f));
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  // exact (erf) GELU, as torch.nn.functional.gelu(approximate="none")
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float softplus_f(float x) {
+  // torch.nn.functional.softplus(beta=1, threshold=20)
+  return x > 20.0f ? x : log1pf(__expf(x));
+}
+
+// unpack 8 bf16 held in a uint4 into floats
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}

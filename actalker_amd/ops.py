@@ -1,0 +1,424 @@
+"""Torch-tensor front end of the C ABI (libactalker_hip.so).
+
+Every function here validates shapes on the host, allocates its output with torch's caching
+allocator (device memory is torch's; compute is ours) and launches on
+``torch.cuda.current_stream()``. Activations are token-major 2-D tensors ``(rows, C)`` in bf16.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+ACT_NONE, ACT_SILU, ACT_GEGLU, ACT_GELU = 0, 1, 2, 3
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need(t: torch.Tensor, dtype, what: str):
+    if not t.is_cuda:
+        raise _lib.ActhError(f"{what}: expected a device tensor, got {t.device}")
+    if t.dtype != dtype:
+        raise _lib.ActhError(f"{what}: expected {dtype}, got {t.dtype}")
+
+
+def _rows(t: torch.Tensor, what: str) -> int:
+    """Row stride (elements) of a 2-D tensor whose rows are contiguous."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise _lib.ActhError(f"{what}: expected a 2-D row-major tensor, got shape {tuple(t.shape)} "
+                             f"strides {t.stride()}")
+    return t.stride(0)
+
+
+# ------------------------------------------------------------------------------------------
+def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optional[torch.Tensor] = None,
+         k1: Optional[int] = None, conv: Optional[dict] = None, temporal: Optional[dict] = None,
+         bias: Optional[torch.Tensor] = None, rowbias: Optional[torch.Tensor] = None, rb_div: int = 1,
+         residual: Optional[torch.Tensor] = None, rmap: Optional[torch.Tensor] = None, r_div: int = 1,
+         r_mod: int = 1, mix: Optional[torch.Tensor] = None, mix_alpha: float = 0.0, alpha: float = 1.0,
+         act: int = ACT_NONE, out: Optional[torch.Tensor] = None, out_f32: bool = False,
+         orow: Optional[Sequence[int]] = None) -> torch.Tensor:
+    """out = epilogue(A . w^T).  ``w``: packed (N, K) bf16.
+
+    A modes: dense (a is (M, K1) [+ a2 (M, K-K1)]), ``conv=dict(H, W, Ho, Wo, stride, upsample, B)``
+    (a is the NHWC image as (B*H*W, C1) [+ a2]), ``temporal=dict(F, S)`` (a is (M, C1) rows).
+    """
+    lib = _lib.load()
+    _need(w, torch.bfloat16, "gemm weight")
+    N, K = w.shape
+    d = _lib.GemmDesc()
+    d.A = a.data_ptr()
+    d.lda = _rows(a, "gemm A")
+    _need(a, torch.bfloat16, "gemm A")
+    c1 = a.shape[1] if k1 is None else k1
+    if a2 is not None:
+        _need(a2, torch.bfloat16, "gemm A2")
+        d.A2 = a2.data_ptr()
+        d.lda2 = _rows(a2, "gemm A2")
+    d.K1 = c1 if a2 is not None else (1 << 30)
+    if conv is not None:
+        cin = c1 + (a2.shape[1] if a2 is not None else 0)
+        d.amode = 1
+        d.H, d.W, d.Ho, d.Wo = conv["H"], conv["W"], conv["Ho"], conv["Wo"]
+        d.conv_stride = conv.get("stride", 1)
+        d.upsample = int(conv.get("upsample", False))
+        d.Cin = cin
+        if K != 9 * cin:
+            raise _lib.ActhError(f"conv gemm: weight K={K} != 9*Cin={9 * cin}")
+        M = conv["B"] * conv["Ho"] * conv["Wo"]
+        d.K1 = c1
+    elif temporal is not None:
+        cin = c1 + (a2.shape[1] if a2 is not None else 0)
+        d.amode = 2
+        d.F, d.S = temporal["F"], temporal["S"]
+        d.Cin = cin
+        if K != 3 * cin:
+            raise _lib.ActhError(f"temporal gemm: weight K={K} != 3*Cin={3 * cin}")
+        M = a.shape[0]
+        d.K1 = c1
+    else:
+        d.amode = 0
+        M = a.shape[0] if M is None else M
+        if a2 is None and a.shape[1] < K:
+            raise _lib.ActhError(f"gemm: A has {a.shape[1]} columns < K={K}")
+    d.B = w.data_ptr()
+    d.ldb = _rows(w, "gemm weight")
+    d.M, d.N, d.K = M, N, K
+    if bias is not None:
+        _need(bias, torch.float32, "gemm bias")
+        d.bias = bias.data_ptr()
+    if rowbias is not None:
+        _need(rowbias, torch.float32, "gemm rowbias")
+        d.rowbias = rowbias.data_ptr()
+        d.rb_div = rb_div
+        d.ldrb = _rows(rowbias, "gemm rowbias")
+    if residual is not None:
+        _need(residual, torch.bfloat16, "gemm residual")
+        d.R = residual.data_ptr()
+        d.ldr = _rows(residual, "gemm residual")
+        if rmap is not None:
+            _need(rmap, torch.int32, "gemm rmap")
+            d.rmap = rmap.data_ptr()
+            d.r_div, d.r_mod = r_div, r_mod
+    if mix is not None:
+        _need(mix, torch.bfloat16, "gemm mix")
+        d.MIX = mix.data_ptr()
+        d.ldmix = _rows(mix, "gemm mix")
+        d.mix_alpha = float(mix_alpha)
+    d.alpha = float(alpha)
+    d.act = act
+    n_out = N // 2 if act == ACT_GEGLU else N
+    if out is None:
+        if orow is not None:
+            raise _lib.ActhError("gemm: orow remap needs an explicit output tensor")
+        out = torch.empty((M, n_out), device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    else:
+        _need(out, torch.float32 if out_f32 else torch.bfloat16, "gemm out")
+    d.out_f32 = int(out_f32)
+    d.C = out.data_ptr()
+    d.ldc = _rows(out, "gemm out")
+    if orow is None:
+        d.orow_div, d.orow_stride, d.orow_off = max(M, 1), max(M, 1), 0
+        if out.shape[0] < M or out.shape[1] < n_out:
+            raise _lib.ActhError(f"gemm: out {tuple(out.shape)} too small for ({M}, {n_out})")
+    else:
+        d.orow_div, d.orow_stride, d.orow_off = orow
+    _lib.check(lib.acth_gemm(ctypes.byref(d), _stream()), "acth_gemm")
+    return out
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor, B: int, H: int, W: int, *, x2=None, stride: int = 1,
+            upsample: bool = False, **kw) -> torch.Tensor:
+    if upsample:
+        Ho, Wo = 2 * H, 2 * W
+    else:
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    return gemm(x, w, a2=x2, conv=dict(B=B, H=H, W=W, Ho=Ho, Wo=Wo, stride=stride, upsample=upsample), **kw)
+
+
+# ------------------------------------------------------------------------------------------
+def flash_attn(qkv: torch.Tensor, nbatch: int, S: int, heads: int, out: Optional[torch.Tensor] = None):
+    """Self-attention over S tokens per batch on fused [q|k|v] rows (nbatch*S, 3C)."""
+    lib = _lib.load()
+    _need(qkv, torch.bfloat16, "flash_attn qkv")
+    C = heads * 64
+    ld = _rows(qkv, "flash_attn qkv")
+    if out is None:
+        out = torch.empty((nbatch * S, C), device=qkv.device, dtype=torch.bfloat16)
+    d = _lib.AttnDesc()
+    base = qkv.data_ptr()
+    d.q, d.k, d.v, d.o = base, base + 2 * C, base + 4 * C, out.data_ptr()
+    d.ldq = d.ldk = d.ldv = ld
+    d.ldo = _rows(out, "flash_attn out")
+    d.bsq = d.bsk = d.bsv = S * ld
+    d.bso = S * d.ldo
+    d.nbatch, d.nheads, d.Sq, d.Skv = nbatch, heads, S, S
+    d.scale = 1.0 / 8.0
+    _lib.check(lib.acth_flash_attn(ctypes.byref(d), _stream()), "acth_flash_attn")
+    return out
+
+
+def temporal_attn(qkv: torch.Tensor, B: int, F: int, S: int, heads: int, out=None):
+    lib = _lib.load()
+    _need(qkv, torch.bfloat16, "temporal_attn qkv")
+    if out is None:
+        out = torch.empty((B * F * S, heads * 64), device=qkv.device, dtype=torch.bfloat16)
+    d = _lib.TemporalAttnDesc()
+    d.qkv, d.ldqkv = qkv.data_ptr(), _rows(qkv, "temporal_attn qkv")
+    d.o, d.ldo = out.data_ptr(), _rows(out, "temporal_attn out")
+    d.B, d.F, d.S, d.H = B, F, S, heads
+    d.scale = 1.0 / 8.0
+    _lib.check(lib.acth_temporal_attn(ctypes.byref(d), _stream()), "acth_temporal_attn")
+    return out
+
+
+def ip_attn(vbase: torch.Tensor, M: int, heads: int, rows_per_ctx: int, S: int, *, q=None, kv=None, nkeys=32,
+            vb=None, mask_a=None, mask_b=None, sa=1.0, sb=1.0, out=None):
+    lib = _lib.load()
+    if out is None:
+        out = torch.empty((M, heads * 64), device=vbase.device, dtype=torch.bfloat16)
+    d = _lib.IpAttnDesc()
+    if kv is not None:
+        d.q, d.ldq = q.data_ptr(), _rows(q, "ip_attn q")
+        d.kv, d.ldkv, d.nkeys = kv.data_ptr(), _rows(kv, "ip_attn kv"), nkeys
+    d.vbase, d.ldvbase = vbase.data_ptr(), _rows(vbase, "ip_attn vbase")
+    if vb is not None:
+        d.vb, d.ldvb = vb.data_ptr(), _rows(vb, "ip_attn vb")
+    if mask_a is not None:
+        _need(mask_a, torch.float32, "ip_attn mask_a")
+        d.mask_a = mask_a.data_ptr()
+    if mask_b is not None:
+        _need(mask_b, torch.float32, "ip_attn mask_b")
+        d.mask_b = mask_b.data_ptr()
+    d.sa, d.sb, d.scale = float(sa), float(sb), 1.0 / 8.0
+    d.out, d.ldo = out.data_ptr(), _rows(out, "ip_attn out")
+    d.M, d.H, d.rows_per_ctx, d.S = M, heads, rows_per_ctx, S
+    _lib.check(lib.acth_ip_attn(ctypes.byref(d), _stream()), "acth_ip_attn")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+def layernorm(x: torch.Tensor, gamma, beta, eps: float = 1e-5, *, add=None, add_div: int = 1,
+              sum_out: Optional[torch.Tensor] = None, out=None):
+    lib = _lib.load()
+    _need(x, torch.bfloat16, "layernorm x")
+    M, C = x.shape
+    if out is None:
+        out = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+    d = _lib.LayerNormDesc()
+    d.x, d.ldx = x.data_ptr(), _rows(x, "layernorm x")
+    if add is not None:
+        d.add, d.ldadd, d.add_div = add.data_ptr(), _rows(add, "layernorm add"), add_div
+        if sum_out is not None:
+            d.sum_out, d.ldsum = sum_out.data_ptr(), _rows(sum_out, "layernorm sum_out")
+    d.gamma = gamma.data_ptr() if gamma is not None else None
+    d.beta = beta.data_ptr() if beta is not None else None
+    d.eps = float(eps)
+    d.y, d.ldy = out.data_ptr(), _rows(out, "layernorm out")
+    d.M, d.C = M, C
+    _lib.check(lib.acth_layernorm(ctypes.byref(d), _stream()), "acth_layernorm")
+    return out
+
+
+def groupnorm(x: torch.Tensor, gamma, beta, eps: float, rows_per_stat: int, *, x2=None, silu=False, groups=32,
+              out=None):
+    lib = _lib.load()
+    _need(x, torch.bfloat16, "groupnorm x")
+    M = x.shape[0]
+    C1 = x.shape[1]
+    C = C1 + (x2.shape[1] if x2 is not None else 0)
+    if out is None:
+        out = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+    ws_bytes = lib.acth_groupnorm_workspace_size(M, C, groups, rows_per_stat)
+    ws = torch.empty((ws_bytes + 7) // 8, device=x.device, dtype=torch.float64)
+    d = _lib.GroupNormDesc()
+    d.x, d.ldx = x.data_ptr(), _rows(x, "groupnorm x")
+    if x2 is not None:
+        d.x2, d.ldx2 = x2.data_ptr(), _rows(x2, "groupnorm x2")
+    d.C1 = C1
+    d.M, d.C, d.G, d.rows_per_stat = M, C, groups, rows_per_stat
+    d.gamma, d.beta, d.eps = gamma.data_ptr(), beta.data_ptr(), float(eps)
+    d.silu = int(silu)
+    d.y, d.ldy = out.data_ptr(), _rows(out, "groupnorm out")
+    d.ws = ws.data_ptr()
+    _lib.check(lib.acth_groupnorm(ctypes.byref(d), _stream()), "acth_groupnorm")
+    return out
+
+
+def mamba_combine_ln(branch_a: dict, branch_e: dict, gamma, beta, eps: float, M: int, S: int, C: int, out=None):
+    """Each branch dict: mode (0 none / 1 identity / 2 pos map), x, y0, y1, L, pos."""
+    lib = _lib.load()
+    if out is None:
+        out = torch.empty((M, C), device=gamma.device, dtype=torch.bfloat16)
+    d = _lib.MambaCombineDesc()
+
+    def fill(pre, br):
+        mode = br["mode"]
+        setattr(d, "mode_" + pre, mode)
+        if br.get("x") is not None:
+            setattr(d, "x" + pre, br["x"].data_ptr())
+            setattr(d, "ldx" + pre, _rows(br["x"], "mamba x"))
+        if mode != 0:
+            setattr(d, "y" + pre + "0", br["y0"].data_ptr())
+            setattr(d, "y" + pre + "1", br["y1"].data_ptr())
+            setattr(d, "ldy" + pre, _rows(br["y0"], "mamba y"))
+            setattr(d, "L" + pre, br["L"])
+        if mode == 2:
+            setattr(d, "pos_" + pre, br["pos"].data_ptr())
+
+    fill("a", branch_a)
+    fill("e", branch_e)
+    d.gamma, d.beta, d.eps = gamma.data_ptr(), beta.data_ptr(), float(eps)
+    d.y, d.ldy = out.data_ptr(), _rows(out, "mamba out")
+    d.M, d.S, d.C = M, S, C
+    _lib.check(lib.acth_mamba_combine_ln(ctypes.byref(d), _stream()), "acth_mamba_combine_ln")
+    return out
+
+
+def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip, *, nb: int, L: int, R: int,
+                   n_keep: int, y0=None, y1=None):
+    """Fused bidirectional scan. u: (nb*L, D) bf16, xdbl: (nb*L, 2*(R+32)) fp32."""
+    lib = _lib.load()
+    _need(u, torch.bfloat16, "scan u")
+    _need(xdbl, torch.float32, "scan xdbl")
+    D = u.shape[1]
+    for t, nm in ((dt_w, "dt_w"), (dt_b, "dt_b"), (A_log, "A_log"), (Dskip, "D")):
+        _need(t, torch.float32, "scan " + nm)
+        if not t.is_contiguous():
+            raise _lib.ActhError(f"scan {nm} must be contiguous")
+    if y0 is None:
+        y0 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
+    if y1 is None:
+        y1 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
+    d = _lib.ScanDesc()
+    d.u, d.ldu = u.data_ptr(), _rows(u, "scan u")
+    d.xdbl, d.ldx = xdbl.data_ptr(), _rows(xdbl, "scan xdbl")
+    d.dt_w, d.dt_b, d.A_log, d.Dskip = dt_w.data_ptr(), dt_b.data_ptr(), A_log.data_ptr(), Dskip.data_ptr()
+    d.y0, d.y1, d.ldy = y0.data_ptr(), y1.data_ptr(), _rows(y0, "scan y0")
+    d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, R, 16, n_keep
+    d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = 1, 2, 0, 0, 1
+    _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
+    return y0, y1
+
+
+def selective_scan_op(u_t: torch.Tensor, delta_t: torch.Tensor, bc: torch.Tensor, A_log: torch.Tensor,
+                      Dskip: Optional[torch.Tensor], delta_bias: Optional[torch.Tensor], *, nb: int, L: int,
+                      G: int, softplus: bool, out: Optional[torch.Tensor] = None):
+    """Generic op mode: u_t (nb*L, G*D) bf16, delta_t (nb*L, G*D) fp32/bf16, bc (nb*L, G*32) fp32
+    [B(16) | C(16)] per group, forward traversal, all L outputs -> (nb*L, G*D) bf16."""
+    lib = _lib.load()
+    _need(u_t, torch.bfloat16, "scan u")
+    _need(bc, torch.float32, "scan B/C")
+    GD = u_t.shape[1]
+    D = GD // G
+    if out is None:
+        out = torch.empty((nb * L, GD), device=u_t.device, dtype=torch.bfloat16)
+    d = _lib.ScanDesc()
+    d.u, d.ldu = u_t.data_ptr(), _rows(u_t, "scan u")
+    d.xdbl, d.ldx = bc.data_ptr(), _rows(bc, "scan B/C")
+    d.dt_b = None if delta_bias is None else delta_bias.data_ptr()
+    d.A_log = A_log.data_ptr()
+    d.Dskip = None if Dskip is None else Dskip.data_ptr()
+    d.y0, d.ldy = out.data_ptr(), _rows(out, "scan out")
+    d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, 0, 16, L
+    d.delta, d.ld_delta = delta_t.data_ptr(), _rows(delta_t, "scan delta")
+    d.delta_f32 = int(delta_t.dtype == torch.float32)
+    d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = int(softplus), G, D, D, 0
+    _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0,
+                       scale: float = 1.0, max_period: float = 10000.0) -> torch.Tensor:
+    lib = _lib.load()
+    t = t.to(torch.float32).contiguous()
+    out = torch.empty((t.numel(), dim), device=t.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_timestep_embedding(_p(t), t.numel(), dim, int(flip_sin_to_cos), shift, scale,
+                                           max_period, _p(out), _stream()), "acth_timestep_embedding")
+    return out
+
+
+def nchw_to_tokens(x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
+    """(B, C, H, W) or (B, F, C, H, W) -> (B*[F*]H*W, C)."""
+    lib = _lib.load()
+    x = x.contiguous()
+    C, H, W = x.shape[-3:]
+    B = x.numel() // (C * H * W)
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    out = torch.empty((B * H * W, C), device=x.device, dtype=out_dtype)
+    _lib.check(lib.acth_nchw_to_tokens(_p(x), int(x.dtype == torch.float32), _p(out),
+                                       int(out_dtype == torch.float32), C, B, C, H * W, _stream()),
+               "acth_nchw_to_tokens")
+    return out
+
+
+def tokens_to_nchw(x: torch.Tensor, B: int, H: int, W: int, out_dtype=torch.float32) -> torch.Tensor:
+    lib = _lib.load()
+    C = x.shape[1]
+    out = torch.empty((B, C, H, W), device=x.device, dtype=out_dtype)
+    _lib.check(lib.acth_tokens_to_nchw(_p(x), int(x.dtype == torch.float32), _rows(x, "tokens"), _p(out),
+                                       int(out_dtype == torch.float32), B, C, H * W, _stream()),
+               "acth_tokens_to_nchw")
+    return out
+
+
+def im2col3x3(x: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
+    lib = _lib.load()
+    C = x.shape[1]
+    K = 9 * C
+    out = torch.empty((B * H * W, K), device=x.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_im2col3x3(_p(x.contiguous()), B, H, W, C, _p(out), K, _stream()), "acth_im2col3x3")
+    return out
+
+
+def gather_rows(src: torch.Tensor, idx: torch.Tensor, nb: int, Ls: int, dst: torch.Tensor, Ld: int):
+    lib = _lib.load()
+    _need(idx, torch.int32, "gather idx")
+    C = src.shape[1]
+    _lib.check(lib.acth_gather_rows(_p(src), _rows(src, "gather src"), Ls, _p(idx), idx.numel(), _p(dst),
+                                    _rows(dst, "gather dst"), Ld, nb, C, _stream()), "acth_gather_rows")
+    return dst
+
+
+def frame_mean(x: torch.Tensor, B: int, F: int, T: int) -> torch.Tensor:
+    """x rows ((b*F + f)*T + t) -> rows (b*T + t), mean over f."""
+    lib = _lib.load()
+    C = x.shape[1]
+    out = torch.empty((B * T, C), device=x.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_frame_mean(_p(x), _rows(x, "frame_mean x"), B, F, T, C, _p(out), C, _stream()),
+               "acth_frame_mean")
+    return out
+
+
+def window_input(lat: torch.Tensor, frame_idx: torch.Tensor, img: torch.Tensor, branch: torch.Tensor,
+                 in_scale: float, U: int, F: int, S: int) -> torch.Tensor:
+    lib = _lib.load()
+    out = torch.empty((U * F * S, 8), device=lat.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_window_input(_p(lat), _p(frame_idx), _p(img), _p(branch), float(in_scale), _p(out),
+                                     U, F, S, _stream()), "acth_window_input")
+    return out
+
+
+def cfg_euler_accum(noise, unit_off, lat, frame_idx, g1, g2, g3, sigma, sigma_next, acc, cnt, F, S):
+    lib = _lib.load()
+    _lib.check(lib.acth_cfg_euler_accum(_p(noise), _p(unit_off), _p(lat), _p(frame_idx), float(g1), float(g2),
+                                        float(g3), float(sigma), float(sigma_next), _p(acc), _p(cnt), F, S,
+                                        _stream()), "acth_cfg_euler_accum")
+
+
+def div_counter(acc, cnt, out, T, S):
+    lib = _lib.load()
+    _lib.check(lib.acth_div_counter(_p(acc), _p(cnt), _p(out), T, S, _stream()), "acth_div_counter")
+    return out

@@ -1,0 +1,418 @@
+"""Drop-in ``UNetSpatioTemporalConditionModel`` for ACTalker's ``unet_cls`` config key.
+
+Reference: src/models/base/unet_spatio_temporal_condition_mambaID_v10_two_ip.py (class at :35,
+``__init__`` :73-251, ``forward`` :362-517, ``add_ip_adapters`` :519-567 — the copy in
+unet_spatio_temporal_condition.py:519-566 without the ``pdb.set_trace()``, and
+``load_adapter_states`` :571-592). Selected by config/inference.yaml:62 via Inference.py:54-62::
+
+    unet_cls: 'actalker_amd.unet_spatio_temporal_condition_mambaID_v10_two_ip.UNetSpatioTemporalConditionModel'
+
+Same constructor arguments, config fields, attribute names, parameter names/shapes and forward
+signature; the forward itself runs on the MI355X kernels of libactalker_hip.so (bf16 activations,
+fp32 accumulation). There is no CPU path: calling forward on a CPU module raises.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .modules import (Attention, AttnProcessor2_0, Conv2d, CrossAttnDownBlockSpatioTemporal,
+                      CrossAttnUpBlockSpatioTemporal, Ctx, DownBlockSpatioTemporal, GroupNorm,
+                      IPAdapterAttnProcessor2_0, Timesteps, TimestepEmbedding,
+                      TransformerSpatioTemporalModel_new_mambaID_v10_two_ip, UNetMidBlockSpatioTemporal,
+                      UpBlockSpatioTemporal)
+
+TransformerSpatioTemporalModel = TransformerSpatioTemporalModel_new_mambaID_v10_two_ip
+
+
+@dataclass
+class UNetSpatioTemporalConditionOutput:
+    sample: torch.Tensor = None
+
+
+class FrozenConfig(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+def get_down_block(down_block_type, num_layers, in_channels, out_channels, temb_channels, add_downsample,
+                   resnet_eps, resnet_act_fn, num_attention_heads, cross_attention_dim=None,
+                   transformer_layers_per_block=1, attn_cls=None, **_):
+    """unet_3d_blocks.py:205-332 (SpatioTemporal branches)."""
+    if down_block_type == "DownBlockSpatioTemporal":
+        return DownBlockSpatioTemporal(num_layers=num_layers, in_channels=in_channels, out_channels=out_channels,
+                                       temb_channels=temb_channels, add_downsample=add_downsample)
+    if down_block_type == "CrossAttnDownBlockSpatioTemporal":
+        if cross_attention_dim is None:
+            raise ValueError("cross_attention_dim must be specified for CrossAttnDownBlockSpatioTemporal")
+        return CrossAttnDownBlockSpatioTemporal(in_channels=in_channels, out_channels=out_channels,
+                                                temb_channels=temb_channels, num_layers=num_layers,
+                                                transformer_layers_per_block=transformer_layers_per_block,
+                                                add_downsample=add_downsample,
+                                                cross_attention_dim=cross_attention_dim,
+                                                num_attention_heads=num_attention_heads, attn_cls=attn_cls)
+    raise ValueError(f"{down_block_type} does not exist.")
+
+
+def get_up_block(up_block_type, num_layers, in_channels, out_channels, prev_output_channel, temb_channels,
+                 add_upsample, resnet_eps, resnet_act_fn, num_attention_heads, resolution_idx=None,
+                 cross_attention_dim=None, transformer_layers_per_block=1, attn_cls=None, **_):
+    """unet_3d_blocks.py:335-473. Note: resnet_eps is NOT forwarded (reference :446-471), so the
+    up blocks keep their 1e-6 default."""
+    if up_block_type == "UpBlockSpatioTemporal":
+        return UpBlockSpatioTemporal(num_layers=num_layers, in_channels=in_channels, out_channels=out_channels,
+                                     prev_output_channel=prev_output_channel, temb_channels=temb_channels,
+                                     resolution_idx=resolution_idx, add_upsample=add_upsample)
+    if up_block_type == "CrossAttnUpBlockSpatioTemporal":
+        if cross_attention_dim is None:
+            raise ValueError("cross_attention_dim must be specified for CrossAttnUpBlockSpatioTemporal")
+        return CrossAttnUpBlockSpatioTemporal(in_channels=in_channels, out_channels=out_channels,
+                                              prev_output_channel=prev_output_channel, temb_channels=temb_channels,
+                                              num_layers=num_layers,
+                                              transformer_layers_per_block=transformer_layers_per_block,
+                                              add_upsample=add_upsample, cross_attention_dim=cross_attention_dim,
+                                              num_attention_heads=num_attention_heads,
+                                              resolution_idx=resolution_idx, attn_cls=attn_cls)
+    raise ValueError(f"{up_block_type} does not exist.")
+
+
+class UNetSpatioTemporalConditionModel(nn.Module):
+    _supports_gradient_checkpointing = True
+
+    def __init__(
+        self,
+        sample_size: Optional[int] = None,
+        in_channels: int = 8,
+        out_channels: int = 4,
+        down_block_types: Tuple[str] = ("CrossAttnDownBlockSpatioTemporal", "CrossAttnDownBlockSpatioTemporal",
+                                        "CrossAttnDownBlockSpatioTemporal", "DownBlockSpatioTemporal"),
+        up_block_types: Tuple[str] = ("UpBlockSpatioTemporal", "CrossAttnUpBlockSpatioTemporal",
+                                      "CrossAttnUpBlockSpatioTemporal", "CrossAttnUpBlockSpatioTemporal"),
+        block_out_channels: Tuple[int] = (320, 640, 1280, 1280),
+        addition_time_embed_dim: int = 256,
+        projection_class_embeddings_input_dim: int = 768,
+        layers_per_block: Union[int, Tuple[int]] = 2,
+        cross_attention_dim: Union[int, Tuple[int]] = 1024,
+        transformer_layers_per_block: Union[int, Tuple[int], Tuple[Tuple]] = 1,
+        num_attention_heads: Union[int, Tuple[int]] = (5, 10, 20, 20),
+        num_frames: int = 25,
+        attn_cls: nn.Module = TransformerSpatioTemporalModel,
+        **_ignored,
+    ):
+        super().__init__()
+        self.config = FrozenConfig(
+            sample_size=sample_size, in_channels=in_channels, out_channels=out_channels,
+            down_block_types=tuple(down_block_types), up_block_types=tuple(up_block_types),
+            block_out_channels=tuple(block_out_channels), addition_time_embed_dim=addition_time_embed_dim,
+            projection_class_embeddings_input_dim=projection_class_embeddings_input_dim,
+            layers_per_block=layers_per_block, cross_attention_dim=cross_attention_dim,
+            transformer_layers_per_block=transformer_layers_per_block, num_attention_heads=num_attention_heads,
+            num_frames=num_frames)
+        self.sample_size = sample_size
+        if len(down_block_types) != len(up_block_types):
+            raise ValueError("Must provide the same number of `down_block_types` as `up_block_types`.")
+        if len(block_out_channels) != len(down_block_types):
+            raise ValueError("Must provide the same number of `block_out_channels` as `down_block_types`.")
+        if not isinstance(num_attention_heads, int) and len(num_attention_heads) != len(down_block_types):
+            raise ValueError("Must provide the same number of `num_attention_heads` as `down_block_types`.")
+        if isinstance(cross_attention_dim, list) and len(cross_attention_dim) != len(down_block_types):
+            raise ValueError("Must provide the same number of `cross_attention_dim` as `down_block_types`.")
+        if not isinstance(layers_per_block, int) and len(layers_per_block) != len(down_block_types):
+            raise ValueError("Must provide the same number of `layers_per_block` as `down_block_types`.")
+
+        self.conv_in = Conv2d(in_channels, block_out_channels[0], kernel_size=3, padding=1)
+        time_embed_dim = block_out_channels[0] * 4
+        self.time_proj = Timesteps(block_out_channels[0], True, downscale_freq_shift=0)
+        self.time_embedding = TimestepEmbedding(block_out_channels[0], time_embed_dim)
+        self.add_time_proj = Timesteps(addition_time_embed_dim, True, downscale_freq_shift=0)
+        self.add_embedding = TimestepEmbedding(projection_class_embeddings_input_dim, time_embed_dim)
+
+        self.down_blocks = nn.ModuleList([])
+        self.up_blocks = nn.ModuleList([])
+        if isinstance(num_attention_heads, int):
+            num_attention_heads = (num_attention_heads,) * len(down_block_types)
+        if isinstance(cross_attention_dim, int):
+            cross_attention_dim = (cross_attention_dim,) * len(down_block_types)
+        if isinstance(layers_per_block, int):
+            layers_per_block = [layers_per_block] * len(down_block_types)
+        if isinstance(transformer_layers_per_block, int):
+            transformer_layers_per_block = [transformer_layers_per_block] * len(down_block_types)
+
+        output_channel = block_out_channels[0]
+        for i, down_block_type in enumerate(down_block_types):
+            input_channel = output_channel
+            output_channel = block_out_channels[i]
+            is_final_block = i == len(block_out_channels) - 1
+            self.down_blocks.append(get_down_block(
+                down_block_type, num_layers=layers_per_block[i],
+                transformer_layers_per_block=transformer_layers_per_block[i], in_channels=input_channel,
+                out_channels=output_channel, temb_channels=time_embed_dim, add_downsample=not is_final_block,
+                resnet_eps=1e-5, cross_attention_dim=cross_attention_dim[i],
+                num_attention_heads=num_attention_heads[i], resnet_act_fn="silu", attn_cls=attn_cls))
+
+        self.mid_block = UNetMidBlockSpatioTemporal(
+            block_out_channels[-1], temb_channels=time_embed_dim,
+            transformer_layers_per_block=transformer_layers_per_block[-1],
+            cross_attention_dim=cross_attention_dim[-1], num_attention_heads=num_attention_heads[-1])
+
+        self.num_upsamplers = 0
+        rev_ch = list(reversed(block_out_channels))
+        rev_heads = list(reversed(num_attention_heads))
+        rev_layers = list(reversed(layers_per_block))
+        rev_cross = list(reversed(cross_attention_dim))
+        rev_tl = list(reversed(transformer_layers_per_block))
+        output_channel = rev_ch[0]
+        for i, up_block_type in enumerate(up_block_types):
+            is_final_block = i == len(block_out_channels) - 1
+            prev_output_channel = output_channel
+            output_channel = rev_ch[i]
+            input_channel = rev_ch[min(i + 1, len(block_out_channels) - 1)]
+            add_upsample = not is_final_block
+            if add_upsample:
+                self.num_upsamplers += 1
+            self.up_blocks.append(get_up_block(
+                up_block_type, num_layers=rev_layers[i] + 1, transformer_layers_per_block=rev_tl[i],
+                in_channels=input_channel, out_channels=output_channel, prev_output_channel=prev_output_channel,
+                temb_channels=time_embed_dim, add_upsample=add_upsample, resnet_eps=1e-5, resolution_idx=i,
+                cross_attention_dim=rev_cross[i], num_attention_heads=rev_heads[i], resnet_act_fn="silu",
+                attn_cls=attn_cls))
+
+        self.conv_norm_out = GroupNorm(num_channels=block_out_channels[0], num_groups=32, eps=1e-5)
+        self.conv_act = nn.SiLU()
+        self.conv_out = Conv2d(block_out_channels[0], out_channels, kernel_size=3, padding=1)
+
+    # -------------------------------------------------------------------------------- API
+    @property
+    def dtype(self) -> torch.dtype:
+        return self.conv_in.weight.dtype
+
+    @property
+    def device(self) -> torch.device:
+        return self.conv_in.weight.device
+
+    @property
+    def attn_processors(self) -> Dict[str, nn.Module]:
+        out = {}
+        for name, mod in self.named_modules():
+            if isinstance(mod, Attention):
+                out[f"{name}.processor"] = mod.processor
+        return out
+
+    def set_attn_processor(self, processor):
+        count = len(self.attn_processors)
+        if isinstance(processor, dict) and len(processor) != count:
+            raise ValueError(f"A dict of processors was passed, but the number of processors {len(processor)} "
+                             f"does not match the number of attention layers: {count}.")
+        for name, mod in self.named_modules():
+            if isinstance(mod, Attention):
+                mod.set_processor(processor if not isinstance(processor, dict) else processor[f"{name}.processor"])
+
+    def set_default_attn_processor(self):
+        self.set_attn_processor(AttnProcessor2_0())
+
+    def invalidate_kernel_cache(self):
+        """Drop every packed kernel-layout weight (call after mutating parameters in place)."""
+        for m in self.modules():
+            if hasattr(m, "_acth_invalidate"):
+                m._acth_invalidate()
+
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        self.invalidate_kernel_cache()
+        return r
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        r = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.invalidate_kernel_cache()
+        return r
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path, subfolder: Optional[str] = None,
+                        variant: Optional[str] = None, **kwargs):
+        """Local-directory loader for a diffusers UNet folder (config.json + safetensors/bin weights).
+        Keys absent from the checkpoint (Mamba / IP-adapter) keep their initialisation, like
+        diffusers' ``low_cpu_mem_usage=False`` path used at Inference.py:56-62."""
+        root = pretrained_model_name_or_path if subfolder is None else os.path.join(pretrained_model_name_or_path,
+                                                                                      subfolder)
+        if not os.path.isdir(root):
+            raise OSError(f"{root} is not a local directory (no network access in this build)")
+        with open(os.path.join(root, "config.json")) as f:
+            cfg = {k: v for k, v in json.load(f).items() if not k.startswith("_")}
+        model = cls(**cfg)
+        stem = "diffusion_pytorch_model"
+        names = ([f"{stem}.{variant}.safetensors", f"{stem}.{variant}.bin"] if variant else []) + \
+                [f"{stem}.safetensors", f"{stem}.bin"]
+        for n in names:
+            p = os.path.join(root, n)
+            if os.path.exists(p):
+                if p.endswith(".safetensors"):
+                    from safetensors.torch import load_file
+                    sd = load_file(p)
+                else:
+                    sd = torch.load(p, map_location="cpu", weights_only=True)
+                model.load_state_dict(sd, strict=False)
+                break
+        else:
+            raise OSError(f"no weights found in {root}")
+        return model
+
+    # -------------------------------------------------------------------------------- forward
+    def _prep_ctx(self, B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs):
+        dev = self.device
+        ctx = Ctx(B, F, dev)
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([float(timestep)], device=dev)
+        t = timestep.reshape(-1).to(dev, torch.float32)
+        if t.numel() == 1:
+            t = t.expand(B).contiguous()
+        t_emb = self.time_proj.run(t)                                          # (B, 320)
+        emb = self.time_embedding.run(t_emb)                                   # (B, 1280)
+        aug = self.add_time_proj.run(added_time_ids.reshape(-1).to(dev, torch.float32))
+        aug = aug.reshape(B, -1)                                               # (B, 768)
+        # silu(emb + aug_emb): the only form in which the ResBlocks consume the embedding
+        ctx.temb = self.add_embedding.run(aug, residual=emb, act_out=ops.ACT_SILU)
+
+        if isinstance(encoder_hidden_states, tuple):
+            id_h, ip = encoder_hidden_states
+        else:
+            id_h, ip = encoder_hidden_states, None
+        if id_h.shape[0] == B:
+            id_h = id_h.repeat_interleave(F, dim=0)
+        ctx.id_tok = id_h.reshape(B * F, -1).to(dev, torch.bfloat16).contiguous()
+        if ip is not None:
+            a, v = ip[0], ip[1]
+            ctx.n_audio = a.shape[-2]
+            ctx.audio_tok = a.reshape(B * F * ctx.n_audio, -1).to(dev, torch.bfloat16).contiguous()
+            ctx.vasa_tok = v.reshape(B * F, -1).to(dev, torch.bfloat16).contiguous()
+            ctx.audio_mean = ops.frame_mean(ctx.audio_tok, B, F, ctx.n_audio)
+            ctx.vasa_mean = ops.frame_mean(ctx.vasa_tok, B, F, 1)
+        else:
+            ctx.has_ip = False
+        ctx.id_mean = ops.frame_mean(ctx.id_tok, B, F, 1)
+        cak = cross_attention_kwargs or {}
+        ctx.masks = cak.get("ip_adapter_masks")
+        gate = cak.get("acth_gate")       # optional hint from actalker_amd.pipeline: exact-zero branches
+        if gate is not None:
+            ctx.audio_zero, ctx.vasa_zero = gate[0] == 0, gate[1] == 0
+        return ctx
+
+    def forward_tokens(self, x_tok: torch.Tensor, B: int, F: int, H: int, W: int, timestep, encoder_hidden_states,
+                       added_time_ids, spatial_condition_tok: Optional[torch.Tensor] = None,
+                       cross_attention_kwargs: Optional[Dict[str, Any]] = None,
+                       spatial_condition_rmap: Optional[torch.Tensor] = None, out_f32: bool = True):
+        """Token-major entry: x_tok (B*F*H*W, in_channels) bf16 -> (B*F*H*W, out_channels)."""
+        if self.device.type != "cuda":
+            raise RuntimeError("UNetSpatioTemporalConditionModel (actalker_amd) runs on the MI355X HIP kernels "
+                               "only; move it to a GPU device first")
+        ctx = self._prep_ctx(B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs)
+        BF = B * F
+        S0 = H * W
+        # conv_in (+ spatial_condition add fused as the residual)
+        cols = ops.im2col3x3(x_tok, BF, H, W)
+        kw = {}
+        if spatial_condition_tok is not None:
+            kw = dict(residual=spatial_condition_tok)
+            if spatial_condition_rmap is not None:
+                kw.update(rmap=spatial_condition_rmap, r_div=S0, r_mod=F)
+        h = ops.gemm(cols, self._conv_in_w(), bias=self.conv_in.b(), **kw)
+        del cols
+        skips = [h]
+        for blk in self.down_blocks:
+            h, outs, H, W = blk.run(ctx, h, H, W)
+            skips.extend(outs)
+        h = self.mid_block.run(ctx, h, H, W)
+        for blk in self.up_blocks:
+            h, H, W = blk.run(ctx, h, skips, H, W)
+        g, b = self.conv_norm_out.gb()
+        n = ops.groupnorm(h, g, b, self.conv_norm_out.eps, H * W, silu=True)
+        return ops.conv3x3(n, self.conv_out.w3(), BF, H, W, bias=self.conv_out.b(), out_f32=out_f32)
+
+    def _conv_in_w(self):
+        # conv_in has Cin = 8 < 64: explicit im2col + dense GEMM, weight as (Cout, 9*Cin)
+        return self.conv_in.w3()
+
+    def forward(self, sample: torch.Tensor, timestep: Union[torch.Tensor, float, int], encoder_hidden_states,
+                added_time_ids: torch.Tensor, spatial_condition: Optional[torch.Tensor] = None,
+                cross_attention_kwargs: Optional[Dict[str, Any]] = None, return_dict: bool = True):
+        B, F = sample.shape[:2]
+        H, W = sample.shape[-2:]
+        with torch.no_grad():
+            x = ops.nchw_to_tokens(sample.to(self.device))
+            sc = ops.nchw_to_tokens(spatial_condition.to(self.device)) if spatial_condition is not None else None
+            out = self.forward_tokens(x, B, F, H, W, timestep, encoder_hidden_states, added_time_ids, sc,
+                                      cross_attention_kwargs)
+            out = ops.tokens_to_nchw(out, B * F, H, W, out_dtype=torch.float32)
+        out = out.reshape(B, F, *out.shape[1:]).to(sample.dtype)
+        if not return_dict:
+            return (out,)
+        return UNetSpatioTemporalConditionOutput(sample=out)
+
+
+# ------------------------------------------------------------------------------------------
+def add_ip_adapters(unet, num_adapter_embeds=[32, ], scale=[1.0, ]):
+    """unet_spatio_temporal_condition.py:519-566: attn1 -> AttnProcessor2_0, attn2 ->
+    IPAdapterAttnProcessor2_0 whose to_k_ip / to_v_ip start as copies of to_k / to_v."""
+    assert len(num_adapter_embeds) == len(scale)
+    attn_procs = {}
+    unet_sd = unet.state_dict()
+    for name in unet.attn_processors.keys():
+        cross_attention_dim = None if name.endswith("attn1.processor") else unet.config.cross_attention_dim
+        if name.startswith("mid_block"):
+            hidden_size = unet.config.block_out_channels[-1]
+        elif name.startswith("up_blocks"):
+            block_id = int(name[len("up_blocks.")])
+            hidden_size = list(reversed(unet.config.block_out_channels))[block_id]
+        elif name.startswith("down_blocks"):
+            block_id = int(name[len("down_blocks.")])
+            hidden_size = unet.config.block_out_channels[block_id]
+        if cross_attention_dim is None:
+            attn_procs[name] = AttnProcessor2_0()
+        else:
+            attn_procs[name] = IPAdapterAttnProcessor2_0(hidden_size=hidden_size,
+                                                         cross_attention_dim=cross_attention_dim,
+                                                         num_tokens=num_adapter_embeds, scale=scale
+                                                         ).to(device=unet.device, dtype=unet.dtype)
+            layer_name = name.split(".processor")[0]
+            weights = {}
+            for i in range(len(num_adapter_embeds)):
+                weights[f"to_k_ip.{i}.weight"] = unet_sd[layer_name + ".to_k.weight"]
+                weights[f"to_v_ip.{i}.weight"] = unet_sd[layer_name + ".to_v.weight"]
+            attn_procs[name].load_state_dict(weights)
+    unet.set_attn_processor(attn_procs)
+    return torch.nn.ModuleList([m for m in unet.attn_processors.values()
+                                if isinstance(m, IPAdapterAttnProcessor2_0)])
+
+
+def load_adapter_states(adapter_modules, state_dict_list):
+    """unet_spatio_temporal_condition.py:570-591: merge adapter state dicts, renumbering the
+    adapter index (key field 2) on collisions; loads with strict=False."""
+    assert len(state_dict_list) > 0
+    merged = {}
+    for state_dict in state_dict_list:
+        for k, v in state_dict.items():
+            if k in merged:
+                k_split = k.split('.')
+                idx = int(k_split[2]) + 1
+                k_split[2] = str(idx)
+                new_k = '.'.join(k_split)
+                while new_k in merged:
+                    idx += 1
+                    k_split[2] = str(idx)
+                    new_k = '.'.join(k_split)
+                merged[new_k] = v
+            else:
+                merged[k] = v
+    info = adapter_modules.load_state_dict(merged, strict=False)
+    for m in adapter_modules.modules():
+        if hasattr(m, "_acth_invalidate"):
+            m._acth_invalidate()
+    return info

@@ -1,0 +1,64 @@
+"""CPU: the C-ABI library loads and exports every entry point include/actalker_hip.h declares;
+argument validation rejects bad shapes before any launch (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from actalker_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "actalker_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t)\s+(acth_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 19
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, f"{n} missing from the ctypes binding"
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_struct_layouts_match_header():
+    lib = _lib.load()
+    assert lib.acth_gemm_desc_size() == ctypes.sizeof(_lib.GemmDesc)
+    src = open(HEADER).read()
+    for cname, py in (("ActhGemmDesc", _lib.GemmDesc), ("ActhAttnDesc", _lib.AttnDesc),
+                      ("ActhTemporalAttnDesc", _lib.TemporalAttnDesc), ("ActhIpAttnDesc", _lib.IpAttnDesc),
+                      ("ActhLayerNormDesc", _lib.LayerNormDesc), ("ActhGroupNormDesc", _lib.GroupNormDesc),
+                      ("ActhMambaCombineDesc", _lib.MambaCombineDesc), ("ActhScanDesc", _lib.ScanDesc)):
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, flags=re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        fields = re.findall(r"(\w+)\s*(?:,|;)", body)
+        assert fields == [f[0] for f in py._fields_], cname
+
+
+def test_invalid_arguments_rejected_without_launch():
+    lib = _lib.load()
+    d = _lib.GemmDesc()
+    assert lib.acth_gemm(ctypes.byref(d), None) == -1               # null operands
+    d.A, d.B, d.C = 16, 16, 16
+    d.M, d.N, d.K, d.lda, d.ldb, d.ldc = 8, 8, 12, 16, 16, 8           # K % 8 != 0
+    assert lib.acth_gemm(ctypes.byref(d), None) == -1
+    s = _lib.ScanDesc()
+    s.u, s.xdbl, s.A_log, s.y0, s.dt_w = 16, 16, 16, 16, 16
+    s.N, s.R, s.L, s.D, s.nb, s.G, s.ldx, s.ldu = 8, 4, 10, 64, 1, 2, 128, 64       # N != 16
+    assert lib.acth_selective_scan(ctypes.byref(s), None) == -1
+    a = _lib.TemporalAttnDesc()
+    a.qkv, a.o, a.F, a.B, a.S, a.H = 16, 16, 17, 1, 1, 1                   # F > 16
+    assert lib.acth_temporal_attn(ctypes.byref(a), None) == -1
+
+
+def test_no_cpu_fallback():
+    import torch
+    from actalker_amd import ops
+    with pytest.raises(_lib.ActhError):
+        ops.layernorm(torch.zeros(4, 8, dtype=torch.bfloat16), None, None)

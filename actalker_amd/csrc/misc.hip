@@ -181,27 +181,29 @@ extern "C" int acth_frame_mean(const void* x, int ldx, int B, int F, int T, int 
 // ------------------------------------------------------------------------------------------
 // UNet input for a batch of units (unit u = one CFG branch of one window):
 //   out[(u*F + f)*S + s, 0:4] = latents[frame_idx[u*F + f]*S + s, 0:4] * in_scale
-//   out[(u*F + f)*S + s, 4:8] = img_lat[branch[u]*S + s, 0:4]
-// latents: fp32 token-major (T*S, 4); img_lat: fp32 (nbranch*S, 4); out bf16 (., 8)
+//   out[(u*F + f)*S + s, 4:8] = img_lat[(branch[u]*T + frame_idx[u*F + f])*S + s, 0:4]
+// latents: fp32 token-major (T*S, 4); img_lat: fp32 (nbranch*T*S, 4); out bf16 (., 8)
 __global__ void window_input_kernel(const float* lat, const int* frame_idx, const float* img,
-                                    const int* branch, float in_scale, bf16_t* out, int U, int F, int S) {
+                                    const int* branch, float in_scale, bf16_t* out, int U, int F, int S,
+                                    int T) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long long)U * F * S) return;
   const int s = (int)(idx % S);
   const long long uf = idx / S;
   const int u = (int)(uf / F);
   const float4 a = *reinterpret_cast<const float4*>(lat + ((size_t)frame_idx[uf] * S + s) * 4);
-  const float4 g = *reinterpret_cast<const float4*>(img + ((size_t)branch[u] * S + s) * 4);
+  const float4 g =
+      *reinterpret_cast<const float4*>(img + (((size_t)branch[u] * T + frame_idx[uf]) * S + s) * 4);
   float v[8] = {a.x * in_scale, a.y * in_scale, a.z * in_scale, a.w * in_scale, g.x, g.y, g.z, g.w};
   *reinterpret_cast<uint4*>(out + idx * 8) = pack8(v);
 }
 
 extern "C" int acth_window_input(const float* lat, const int* frame_idx, const float* img, const int* branch,
-                                 float in_scale, void* out, int U, int F, int S, hipStream_t stream) {
-  if (!lat || !frame_idx || !img || !branch || !out || U <= 0 || F <= 0 || S <= 0) return ACTH_EINVAL;
+                                 float in_scale, void* out, int U, int F, int S, int T, hipStream_t stream) {
+  if (!lat || !frame_idx || !img || !branch || !out || U <= 0 || F <= 0 || S <= 0 || T <= 0) return ACTH_EINVAL;
   const long long n = (long long)U * F * S;
   hipLaunchKernelGGL(window_input_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, lat,
-                     frame_idx, img, branch, in_scale, (bf16_t*)out, U, F, S);
+                     frame_idx, img, branch, in_scale, (bf16_t*)out, U, F, S, T);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -300,6 +300,8 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
         y0 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
     if y1 is None:
         y1 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
+    if n_keep == 0:
+        return y0, y1
     d = _lib.ScanDesc()
     d.u, d.ldu = u.data_ptr(), _rows(u, "scan u")
     d.xdbl, d.ldx = xdbl.data_ptr(), _rows(xdbl, "scan xdbl")
@@ -403,11 +405,12 @@ def frame_mean(x: torch.Tensor, B: int, F: int, T: int) -> torch.Tensor:
 
 
 def window_input(lat: torch.Tensor, frame_idx: torch.Tensor, img: torch.Tensor, branch: torch.Tensor,
-                 in_scale: float, U: int, F: int, S: int) -> torch.Tensor:
+                 in_scale: float, U: int, F: int, S: int, T: int) -> torch.Tensor:
+    """lat (T*S, 4) fp32, img (nbranch*T*S, 4) fp32 -> (U*F*S, 8) bf16 UNet input."""
     lib = _lib.load()
     out = torch.empty((U * F * S, 8), device=lat.device, dtype=torch.bfloat16)
     _lib.check(lib.acth_window_input(_p(lat), _p(frame_idx), _p(img), _p(branch), float(in_scale), _p(out),
-                                     U, F, S, _stream()), "acth_window_input")
+                                     U, F, S, T, _stream()), "acth_window_input")
     return out
 
 

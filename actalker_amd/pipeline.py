@@ -1,0 +1,191 @@
+"""The 25-step EulerDiscrete denoising loop, MI355X-native and frame-window sharded over GPUs.
+
+Reference: Pose2VideoLongSVDPipeline.__call__ step x window loop
+(src/pipelines/pipeline_svd_audio_adapter_motionexp_idembed_vasa_two_ip.py:670-756) with diffusers
+0.29.2 EulerDiscreteScheduler (Karras sigmas, v-prediction, continuous timesteps 0.25*ln(sigma);
+mirror src/schedulers/scheduling_euler_discrete.py).
+
+Work decomposition. Within a step every window is independent (overlap = 0 gives disjoint frame
+sets, pipeline:684-751) and so is every CFG branch until guidance (:731-733). A *unit* is one
+(window, CFG branch) pair = one 14-frame UNet batch element. Units are dealt to ranks in contiguous
+blocks (N = 112 -> 9 windows x 4 branches = 36 units -> 5/5/5/5/4/4/4/4 over 8 GPUs); each rank runs
+its units in UNet calls of up to ``units_per_call`` units (4 = one 56-frame batch, the reference's
+call shape), then ONE all-gather of the fp32 noise predictions per step (RCCL over xGMI; torch's
+"nccl" backend is RCCL on ROCm) gives every rank all branches, and every rank applies guidance +
+Euler + window accumulation for all windows (tiny, replicated) so the latent state stays identical
+everywhere without a second collective. Frames of one window never split across ranks (temporal
+attention and the temporal GroupNorm span the window).
+
+State: latents_all is fp32 token-major (T*h*w, 4) on device for the whole loop (the reference keeps
+it in the UNet dtype, pipeline:674-681; fp32 here is strictly more accurate).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+# ------------------------------------------------------------------------------------------ scheduler
+def karras_sigmas(num_inference_steps: int = 25, sigma_min: float = 0.002, sigma_max: float = 700.0,
+                  rho: float = 7.0) -> Tuple[List[float], List[float]]:
+    """EulerDiscreteScheduler.set_timesteps (use_karras_sigmas, timestep_type='continuous',
+    prediction_type='v_prediction'): returns (sigmas[steps+1] with a final 0, timesteps 0.25*ln(sigma))."""
+    ramp = np.linspace(0, 1, num_inference_steps)
+    min_inv = sigma_min ** (1 / rho)
+    max_inv = sigma_max ** (1 / rho)
+    sig = torch.from_numpy((max_inv + ramp * (min_inv - max_inv)) ** rho).to(torch.float32)
+    ts = [float(0.25 * s.log()) for s in sig]
+    return [float(s) for s in sig] + [0.0], ts
+
+
+# ------------------------------------------------------------------------------------------ planning
+def window_frames(T: int, fpb: int, overlap: int, shift: int) -> List[List[int]]:
+    """Frame indices of every window at a step (pipeline:684-694): start - shift, wrapped mod T."""
+    out = []
+    for index_start in range(0, T, fpb - overlap):
+        s = index_start - shift
+        out.append([(s + j) % T for j in range(fpb)])
+    return out
+
+
+def assign_units(n_windows: int, world: int, rank: int, n_branch: int = 4) -> Tuple[List[Tuple[int, int]], int]:
+    """Contiguous block of (window, branch) units for ``rank``; also returns the per-rank capacity
+    (max units on any rank) used to size the all-gather."""
+    n = n_windows * n_branch
+    cap = math.ceil(n / world)
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    count = base + (1 if rank < extra else 0)
+    units = [(u // n_branch, u % n_branch) for u in range(start, start + count)]
+    return units, cap
+
+
+def unit_owner(n_windows: int, world: int, n_branch: int = 4) -> List[Tuple[int, int]]:
+    """For every global unit u = window*n_branch + branch: (rank, slot within that rank)."""
+    owners = []
+    for r in range(world):
+        units, _ = assign_units(n_windows, world, r, n_branch)
+        for slot, (w, c) in enumerate(units):
+            owners.append((r, slot))
+    return owners
+
+
+# ------------------------------------------------------------------------------------------ backend
+class HipBackend:
+    """Runs units through the HIP UNet (forward_tokens) and the fused guidance/Euler kernel."""
+
+    def __init__(self, unet, H: int, W: int, masks, gate, added_time_ids: torch.Tensor, T: int, fpb: int,
+                 image_latents, image_embeddings, audio_prompts, vasa_prompts, pose_fea):
+        from . import ops
+        self.ops = ops
+        self.unet = unet
+        dev = unet.device
+        self.dev = dev
+        self.H, self.W, self.S = H, W, H * W
+        self.T, self.F = T, fpb
+        self.masks = masks
+        self.gate = list(gate)
+        nb = image_latents.shape[0]
+        # conditioning in device layouts, converted once per run
+        self.img = ops.nchw_to_tokens(image_latents.to(dev).float(), out_dtype=torch.float32)     # (nb*T*S, 4)
+        self.ide = image_embeddings.to(dev, torch.bfloat16).reshape(nb, T, -1)                    # (nb, T, 1024)
+        self.aud = (audio_prompts.to(dev, torch.float32) * self.gate[0]).to(torch.bfloat16)        # (nb, T, 32, 1024)
+        self.n_audio = self.aud.shape[2]
+        self.vas = (vasa_prompts.to(dev, torch.float32) * self.gate[1]).to(torch.bfloat16).reshape(nb, T, -1)
+        self.pose = ops.nchw_to_tokens(pose_fea.to(dev))                                            # (T*S, 320)
+        self.added = added_time_ids.to(dev, torch.float32)                                          # (nb, 3)
+
+    def new_state(self, latents_all: torch.Tensor) -> torch.Tensor:
+        return self.ops.nchw_to_tokens(latents_all.to(self.dev).float(), out_dtype=torch.float32)  # (T*S, 4)
+
+    def run_units(self, lat: torch.Tensor, units: Sequence[Tuple[int, int]], frames: List[List[int]],
+                  t: float, sigma: float, out: torch.Tensor, row0: int):
+        """UNet on ``units``; noise rows written to out[row0 : row0 + U*F*S]."""
+        ops, F, S = self.ops, self.F, self.S
+        U = len(units)
+        fidx = torch.tensor([f for (w, _c) in units for f in frames[w]], dtype=torch.int32)
+        branch = torch.tensor([c for (_w, c) in units], dtype=torch.int64)
+        fidx_d = fidx.to(self.dev, non_blocking=True)
+        br_d = branch.to(self.dev, non_blocking=True)
+        x = ops.window_input(lat, fidx_d, self.img, br_d.to(torch.int32), 1.0 / math.sqrt(sigma * sigma + 1.0),
+                             U, F, S, self.T)
+        fl = fidx_d.long()
+        bl = br_d.repeat_interleave(F)
+        ehs = (self.ide[bl, fl], [self.aud[bl, fl], self.vas[bl, fl]])
+        cak = {"ip_adapter_masks": self.masks, "acth_gate": self.gate}
+        tt = torch.full((1,), t, device=self.dev, dtype=torch.float32)
+        noise = self.unet.forward_tokens(x, U, F, self.H, self.W, tt, ehs, self.added[br_d], self.pose, cak,
+                                         spatial_condition_rmap=fidx_d, out_f32=True)
+        out[row0:row0 + U * F * S].copy_(noise)
+
+    def step_windows(self, lat, gathered, unit_rows: List[List[int]], frames, guidance, sigma, sigma_next):
+        """Guidance + Euler + accumulate for every window, then average (pipeline:731-756)."""
+        ops = self.ops
+        acc = torch.zeros_like(lat)
+        cnt = torch.zeros(self.T, device=self.dev, dtype=torch.float32)
+        for w, rows in enumerate(unit_rows):
+            offs = torch.tensor(rows, dtype=torch.int64).to(self.dev, non_blocking=True)
+            fidx = torch.tensor(frames[w], dtype=torch.int32).to(self.dev, non_blocking=True)
+            ops.cfg_euler_accum(gathered, offs, lat, fidx, guidance[0], guidance[1], guidance[2], sigma, sigma_next,
+                                acc, cnt, self.F, self.S)
+        return ops.div_counter(acc, cnt, torch.empty_like(lat), self.T, self.S)
+
+    def finish(self, lat: torch.Tensor) -> torch.Tensor:
+        out = self.ops.tokens_to_nchw(lat, self.T, self.H, self.W)
+        return out.reshape(1, self.T, 4, self.H, self.W)
+
+
+# ------------------------------------------------------------------------------------------ loop
+@dataclass
+class LoopConfig:
+    num_frames: int
+    frames_per_batch: int = 14
+    overlap: int = 0
+    shift_offset: int = 7
+    num_inference_steps: int = 25
+    guidance: Tuple[float, float, float] = (2.0, 7.5, 3.0)
+    sigma_min: float = 0.002
+    sigma_max: float = 700.0
+    units_per_call: int = 4
+
+
+def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, world: int = 1,
+            group=None, step_callback: Optional[Callable[[int], None]] = None, steps: Optional[int] = None):
+    """Run the sampler loop. ``latents_all``: (1, T, 4, h, w) (already ``add_noise``d, pipeline:586-598).
+
+    With world > 1, torch.distributed must be initialised; each rank runs its unit block and one
+    ``all_gather_into_tensor`` per step exchanges the noise predictions."""
+    T = cfg.num_frames + cfg.frames_per_batch
+    F = cfg.frames_per_batch
+    sigmas, timesteps = karras_sigmas(cfg.num_inference_steps, cfg.sigma_min, cfg.sigma_max)
+    lat = backend.new_state(latents_all)
+    n_windows = len(range(0, T, F - cfg.overlap))
+    my_units, cap = assign_units(n_windows, world, rank)
+    owners = unit_owner(n_windows, world)
+    S = backend.S
+    rows_per_unit = F * S
+    local = torch.zeros((cap * rows_per_unit, 4), device=lat.device, dtype=torch.float32)
+    gathered = torch.empty((world * cap * rows_per_unit, 4), device=lat.device, dtype=torch.float32) \
+        if world > 1 else local
+    # row offset of every global unit inside the gathered buffer
+    unit_row = [(r * cap + slot) * rows_per_unit for (r, slot) in owners]
+    shift = 0
+    n_steps = cfg.num_inference_steps if steps is None else steps
+    for i in range(n_steps):
+        frames = window_frames(T, F, cfg.overlap, shift)
+        for c0 in range(0, len(my_units), cfg.units_per_call):
+            chunk = my_units[c0:c0 + cfg.units_per_call]
+            backend.run_units(lat, chunk, frames, timesteps[i], sigmas[i], local, c0 * rows_per_unit)
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_gather_into_tensor(gathered, local, group=group)
+        unit_rows = [[unit_row[w * 4 + c] for c in range(4)] for w in range(n_windows)]
+        lat = backend.step_windows(lat, gathered, unit_rows, frames, cfg.guidance, sigmas[i], sigmas[i + 1])
+        shift = (shift + cfg.shift_offset) % F
+        if step_callback is not None:
+            step_callback(i)
+    return backend.finish(lat)

@@ -322,7 +322,8 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         if spatial_condition_tok is not None:
             kw = dict(residual=spatial_condition_tok)
             if spatial_condition_rmap is not None:
-                kw.update(rmap=spatial_condition_rmap, r_div=S0, r_mod=F)
+                # row (u*F + f)*S0 + s reads spatial_condition row rmap[u*F + f]*S0 + s
+                kw.update(rmap=spatial_condition_rmap, r_div=S0, r_mod=spatial_condition_rmap.numel())
         h = ops.gemm(cols, self._conv_in_w(), bias=self.conv_in.b(), **kw)
         del cols
         skips = [h]

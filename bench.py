@@ -1,0 +1,266 @@
+"""Benchmark: denoised frames/sec of ACTalker's 25-step audio-driven denoising at 576x1024, 14 frames
+per GPU (BASELINE.json metric), on 1..8 MI355X with one process per GPU.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+
+A "step" is one sampler step of the loop (pipeline:671): every window x CFG-branch UNet pass
+(2 x 56-frame calls at N=14 on one GPU) + guidance + Euler + window accumulation. The sampler's
+steps are shape-identical, so frames/sec = N_frames / (25 * seconds_per_step). Weak scaling: each GPU
+adds 14 output frames (N = 14 * world), units = (window, CFG branch) sharded contiguously, one RCCL
+all-gather of noise predictions per step.
+
+Synthetic data: seed 72589, latents/tokens ~N(0,1), pose ~N(0,0.1), masks per
+mode, added_time_ids [12.5, 12, 20], guidance 2.0/7.5/3.0, shift 7, overlap 0; random-init weights of
+the full SVD-XT + ACTalker v10 architecture (1.775 B params, no checkpoints offline).
+
+Also reported: the dominant kernel's roofline (HIP events around its launches inside the timed
+region) and the CPU baseline (the oracle restatement, fp32, on this host's cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+TFLOP_PER_FRAME_FWD = 3.433        # SURVEY.md 8(d), 576x1024, mode 2 (modes 0/1: 3.402)
+MODES = {0: ([1, 0], "mode=0 audio-only"), 1: ([0, 1], "mode=1 expression-only"), 2: ([1, 1], "mode=2 audio+expression")}
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_unet(device, seed=72589):
+    from actalker_amd.synthetic import init_synthetic_
+    from actalker_amd.unet_spatio_temporal_condition_mambaID_v10_two_ip import (UNetSpatioTemporalConditionModel,
+                                                                               add_ip_adapters)
+    with torch.device("meta"):
+        unet = UNetSpatioTemporalConditionModel(num_frames=25)
+    unet = unet.to_empty(device="cpu")
+    add_ip_adapters(unet, [32, 32], [1.25, 1.25])
+    init_synthetic_(unet, seed)
+    return unet
+
+
+def synthetic_inputs(N, fpb, H, W, mode, seed=72589):
+    """Pipeline-internal tensors after CFG stacking (pipeline:128-184, 522-598, 636-638)."""
+    g = torch.Generator().manual_seed(seed)
+    T = N + fpb
+    h, w = H // 8, W // 8
+    ref_lat = torch.randn(1, 4, h, w, generator=g)
+    noise = torch.randn(1, T, 4, h, w, generator=g)
+    img_lat = torch.randn(1, 4, h, w, generator=g)
+    id_tok = torch.randn(1, 1, 1024, generator=g)
+    audio = torch.randn(N, 32, 1024, generator=g)
+    uncond_audio = torch.randn(32, 1024, generator=g)
+    vasa = torch.randn(N, 1024, generator=g) if mode != 0 else torch.zeros(N, 1024)
+    uncond_vasa = torch.randn(1024, generator=g) if mode != 0 else torch.zeros(1024)
+    pose = 0.1 * torch.randn(1, T, 320, h, w, generator=g)
+    # CFG stacks: ID [0, id, id, id]; audio [u, u, a, a]; vasa [u, u, u, v]; +fpb uncond pad frames
+    ide = torch.cat([torch.zeros(1, T, 1, 1024)] + [id_tok[:, None].expand(1, T, 1, 1024)] * 3)
+    a_c = torch.cat([audio, uncond_audio[None].expand(fpb, 32, 1024)])[None]
+    a_u = uncond_audio[None, None].expand(1, T, 32, 1024)
+    aud = torch.cat([a_u, a_u, a_c, a_c])
+    v_c = torch.cat([vasa, uncond_vasa[None].expand(fpb, 1024)])[None, :, None]
+    v_u = uncond_vasa[None, None, None].expand(1, T, 1, 1024)
+    vas = torch.cat([v_u, v_u, v_u, v_c])
+    imgl = torch.cat([torch.zeros(1, T, 4, h, w)] + [img_lat[:, None].expand(1, T, 4, h, w)] * 3)
+    sigma0 = 700.0
+    latents = 0.18215 * ref_lat[:, None] + sigma0 * noise                 # scheduler.add_noise at t0
+    added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
+    ones = torch.ones(1, 1, H, W)
+    masks = [ones, ones]                                                 # face mask = all ones (no face model)
+    return dict(latents=latents, image_latents=imgl.contiguous(), image_embeddings=ide.contiguous(),
+                audio_prompts=aud.contiguous(), vasa_prompts=vas.contiguous(), pose_fea=pose, added=added,
+                masks=masks)
+
+
+class GemmTimer:
+    """HIP events around every GEMM launch on the launch stream (torch's current stream)."""
+
+    def __init__(self):
+        self.events = []
+        self.flops = 0.0
+        self.launches = 0
+
+    def install(self):
+        from actalker_amd import ops
+        orig = ops.gemm
+        self.orig = orig
+
+        def timed(a, w, **kw):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            out = orig(a, w, **kw)
+            e1.record()
+            N, K = w.shape
+            M = out.shape[0] if kw.get("orow") is None else (kw.get("M") or a.shape[0])
+            if kw.get("conv") is not None:
+                c = kw["conv"]
+                M = c["B"] * c["Ho"] * c["Wo"]
+            elif kw.get("M") is not None:
+                M = kw["M"]
+            else:
+                M = a.shape[0]
+            self.flops += 2.0 * M * N * K
+            self.launches += 1
+            self.events.append((e0, e1))
+            return out
+        ops.gemm = timed
+        import actalker_amd.modules as mods
+        mods.ops = ops
+        return self
+
+    def uninstall(self):
+        from actalker_amd import ops
+        ops.gemm = self.orig
+
+    def total_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.events)
+
+
+def cpu_baseline(unet, H, W, frames=2, mode=0):
+    """Oracle (fp32 CPU restatement) on a bounded sample: one UNet call, 1 CFG branch x `frames`
+    frames at full resolution; frames/s extrapolated to the N=14 workload (200 frame-forwards
+    per output frame = 4 CFG x 25 steps x 28/14)."""
+    from oracle import reference_cpu as ref
+    sd = {k: v.detach().float().cpu() for k, v in unet.state_dict().items()}
+    g = torch.Generator().manual_seed(1)
+    h, w = H // 8, W // 8
+    sample = torch.randn(1, frames, 8, h, w, generator=g)
+    ehs = (torch.randn(frames, 1, 1024, generator=g),
+           [torch.randn(frames, 32, 1024, generator=g), torch.randn(frames, 1, 1024, generator=g) * (mode != 0)])
+    pose = 0.1 * torch.randn(1, frames, 320, h, w, generator=g)
+    masks = [torch.ones(1, 1, H, W), torch.ones(1, 1, H, W) if mode != 0 else torch.zeros(1, 1, H, W)]
+    if mode == 1:
+        masks = [torch.zeros(1, 1, H, W), torch.ones(1, 1, H, W)]
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref.unet_forward(sd, sample, torch.tensor(1.6), ehs, torch.tensor([[12.5, 12.0, 20.0]]), pose,
+                         {"ip_adapter_masks": masks})
+    dt = time.perf_counter() - t0
+    per_frame_fwd = dt / frames
+    fps = 1.0 / (per_frame_fwd * 200.0)
+    return dict(value=fps, unit="frames/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"oracle fp32 UNet call, 1 CFG branch x {frames} frames at {H}x{W} ({dt:.1f} s = "
+                       f"{per_frame_fwd:.2f} s/frame-forward), extrapolated x200 frame-forwards per output frame")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=25, help="timed sampler steps (25 = one full denoise)")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", type=int, default=0, choices=[0, 1, 2])
+    ap.add_argument("--frames-per-gpu", type=int, default=14)
+    ap.add_argument("--height", type=int, default=576)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from actalker_amd import pipeline as pl
+
+    gate, mode_name = MODES[args.mode]
+    N = args.frames_per_gpu * world
+    fpb = 14
+    H, W = args.height, args.width
+    t0 = time.time()
+    unet_cpu = build_unet(dev)
+    unet = unet_cpu.to(dev)
+    log(f"model built in {time.time() - t0:.1f}s")
+    inp = synthetic_inputs(N, fpb, H, W, args.mode)
+    backend = pl.HipBackend(unet, H // 8, W // 8, inp["masks"], gate, inp["added"], N + fpb, fpb,
+                            inp["image_latents"], inp["image_embeddings"], inp["audio_prompts"],
+                            inp["vasa_prompts"], inp["pose_fea"])
+    cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # warmup (packs weights, builds mask tables, warms the allocator)
+    with torch.no_grad():
+        pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.warmup)
+    timer = None if args.no_roofline else GemmTimer().install()
+    barrier()
+    t_start = time.perf_counter()
+    with torch.no_grad():
+        out = pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.steps)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if timer is not None:
+        timer.uninstall()
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = bool(torch.isfinite(out).all())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    fps = N / (cfg.num_inference_steps * elapsed / args.steps)
+
+    roof = None
+    if timer is not None and timer.launches:
+        gemm_ms = timer.total_ms()
+        achieved = timer.flops / (gemm_ms / 1000.0) / 1e12
+        roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                    frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=None, kernel="gemm_bf16_kernel",
+                    launches=timer.launches, avg_launch_us=round(1000.0 * gemm_ms / timer.launches, 2),
+                    kernel_share_of_step=round(gemm_ms / (elapsed * 1000.0), 3))
+    n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank)[0])
+    frame_fwds = n_units_rank * fpb * args.steps
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(unet_cpu, H, W, frames=args.cpu_frames, mode=args.mode)
+    if rank == 0:
+        line = {
+            "metric": "denoised frames/sec, 576x1024x14f x25-step audio-driven, 1/2/4/8 MI355X",
+            "value": round(fps, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"{mode_name}, {H}x{W}, {N} frames ({args.frames_per_gpu}/GPU), fpb {fpb}, "
+                                   f"25-step EulerDiscrete, 4-way CFG, (window x branch) units over {world} GPU(s)",
+                       "model": "SVD-XT UNet + ACTalker v10 dual-Mamba (1.775B, random init)",
+                       "global_batch": N, "seq_len": fpb, "parallelism": f"units{world}"},
+            "unet_frame_forwards_per_s_per_gpu": round(frame_fwds / elapsed, 3),
+            "achieved_mfma_tflops_whole_step": round(frame_fwds * TFLOP_PER_FRAME_FWD / elapsed, 1),
+            "finite": ok,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -156,7 +156,7 @@ int acth_frame_mean(const void* x, int ldx, int B, int F, int T, int C, void* ou
 
 /* ---- sampler loop (pipeline_svd_audio_adapter_motionexp_idembed_vasa_two_ip.py:684-756) */
 int acth_window_input(const float* lat, const int* frame_idx, const float* img, const int* branch,
-                      float in_scale, void* out, int U, int F, int S, hipStream_t stream);
+                      float in_scale, void* out, int U, int F, int S, int T, hipStream_t stream);
 int acth_cfg_euler_accum(const float* noise, const long long* unit_off, const float* lat, const int* frame_idx,
                          float g1, float g2, float g3, float sigma, float sigma_next, float* acc, float* cnt,
                          int F, int S, hipStream_t stream);

@@ -1,0 +1,151 @@
+"""GPU parity of the drop-in modules against the reference's golden vectors and the CPU oracle.
+
+Tolerances (bf16 activations, fp32 accumulation, stated per test):
+  * SS2D_cond_v10 vs the reference module's own outputs: rel-L2 <= 2e-2
+  * UNet forward vs oracle (tiny width, real topology, 3 frames): rel-L2 <= 5e-2
+  * 3 sampler steps of the loop vs the oracle loop: rel-L2 <= 5e-2 on the final latents
+"""
+import os
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+import __graft_entry__ as ge
+from oracle import reference_cpu as ref
+from tests.golden_weights import CASES, golden_weights, make_inputs
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_ss2d_cond_v10_matches_reference_golden(dev, name):
+    from actalker_amd.modules import Ctx, SS2D_cond_v10
+    case = CASES[name]
+    g = load_file(os.path.join(GOLD, f"ss2d_cond_v10_{name}.safetensors"))
+    x, id_emb, conds, masks = make_inputs(case)
+    m = SS2D_cond_v10(d_model=case["d_model"], d_cond=case["d_cond"], cond_size=32, dropout=0.1, d_state=16,
+                      size=8, scan_type="sweep", num_direction=2)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict(golden_weights(case["seed"], shapes), strict=True)
+    m = m.to(dev)
+    BF, S, C = x.shape
+    ctx = Ctx(BF, 1, dev)
+    ctx.id_tok = id_emb.reshape(BF, -1).to(dev, torch.bfloat16)
+    ctx.audio_tok = conds[:, :32].reshape(BF * 32, -1).to(dev, torch.bfloat16)
+    ctx.vasa_tok = conds[:, 32].reshape(BF, -1).to(dev, torch.bfloat16)
+    ctx.masks = masks
+    y = m.run(ctx, x.reshape(BF * S, C).to(dev, torch.bfloat16), S)
+    err = rel(y.view(BF, S, C), g["y"])
+    assert err < 2e-2, err
+
+
+def _oracle_cfg(cfg):
+    return dict(block_out_channels=cfg["block_out_channels"], num_attention_heads=cfg["num_attention_heads"])
+
+
+@pytest.fixture(scope="module")
+def tiny(dev):
+    unet, cfg = ge._tiny_unet(seed=9)
+    sd = {k: v.detach().clone() for k, v in unet.state_dict().items()}
+    return unet.to(dev), sd, cfg
+
+
+@pytest.mark.parametrize("masks_kind", ["mode2", "mode0", "mode1", "half"])
+def test_unet_forward_matches_oracle(dev, tiny, masks_kind):
+    unet, sd, cfg = tiny
+    sample, t, ehs, added, pose, _ = ge._tiny_inputs(B=2, F=3, H=16, W=32, seed=4)
+    H8, W8 = 128, 256
+    one, zero = torch.ones(1, 1, H8, W8), torch.zeros(1, 1, H8, W8)
+    lower = zero.clone()
+    lower[..., H8 // 2:, :] = 1.0
+    masks = {"mode2": [one, one], "mode0": [one, zero], "mode1": [zero, one], "half": [lower, 1 - lower]}[masks_kind]
+    if masks_kind == "mode0":
+        ehs = (ehs[0], [ehs[1][0], torch.zeros_like(ehs[1][1])])
+    if masks_kind == "mode1":
+        ehs = (ehs[0], [torch.zeros_like(ehs[1][0]), ehs[1][1]])
+    cak = {"ip_adapter_masks": masks}
+    out = unet(sample.to(dev), t.to(dev), (ehs[0].to(dev), [e.to(dev) for e in ehs[1]]), added.to(dev),
+               spatial_condition=pose.to(dev), cross_attention_kwargs=cak, return_dict=False)[0]
+    want = ref.unet_forward(sd, sample, t, ehs, added, pose, cak, ip_scale=(1.25, 1.25), cfg=_oracle_cfg(cfg))
+    err = rel(out, want)
+    assert err < 5e-2, err
+
+
+def test_unet_gate_hint_is_exact(dev, tiny):
+    """The pipeline's gate hint only skips work whose result is exactly zero."""
+    unet, sd, cfg = tiny
+    sample, t, ehs, added, pose, masks = ge._tiny_inputs(B=1, F=3, H=16, W=32, seed=5)
+    ehs = (ehs[0], [ehs[1][0], torch.zeros_like(ehs[1][1])])
+    masks = [masks[0], torch.zeros_like(masks[1])]
+    args = (sample.to(dev), t.to(dev), (ehs[0].to(dev), [e.to(dev) for e in ehs[1]]), added.to(dev))
+    a = unet(*args, spatial_condition=pose.to(dev), cross_attention_kwargs={"ip_adapter_masks": masks},
+             return_dict=False)[0]
+    b = unet(*args, spatial_condition=pose.to(dev),
+             cross_attention_kwargs={"ip_adapter_masks": masks, "acth_gate": [1, 0]}, return_dict=False)[0]
+    assert rel(a, b) < 1e-3
+
+
+def test_pipeline_loop_matches_oracle(dev, tiny):
+    """3 sampler steps of the windowed 4-way-CFG loop (N=4 frames, window 2, shift 1) vs the oracle."""
+    from actalker_amd import pipeline as pl
+    unet, sd, cfg = tiny
+    N, fpb, H, W = 4, 2, 16, 32
+    T = N + fpb
+    g = torch.Generator().manual_seed(21)
+    latents = 0.18215 * torch.randn(1, 1, 4, H, W, generator=g) + 700.0 * torch.randn(1, T, 4, H, W, generator=g)
+    imgl = torch.randn(4, T, 4, H, W, generator=g)
+    imgl[0] = 0
+    ide = torch.randn(4, T, 1, 1024, generator=g)
+    aud = torch.randn(4, T, 32, 1024, generator=g)
+    vas = torch.randn(4, T, 1, 1024, generator=g)
+    pose = 0.1 * torch.randn(1, T, 64, H, W, generator=g)
+    added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
+    masks = [torch.ones(1, 1, 8 * H, 8 * W), torch.ones(1, 1, 8 * H, 8 * W)]
+    gate = [1, 1]
+    lc = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, num_inference_steps=25)
+    backend = pl.HipBackend(unet, H, W, masks, gate, added, T, fpb, imgl, ide, aud, vas, pose)
+    with torch.no_grad():
+        got = pl.denoise(backend, latents, lc, steps=3)
+
+    def unet_fn(sample, t, ehs, added_ids, sc, cak):
+        return ref.unet_forward(sd, sample, t, ehs, added_ids, sc, cak, ip_scale=(1.25, 1.25),
+                                cfg=_oracle_cfg(cfg))
+
+    want = _oracle_loop(unet_fn, latents, imgl, ide, aud, vas, pose, added, masks, gate, N, fpb, steps=3)
+    err = rel(got, want)
+    assert err < 5e-2, err
+
+
+def _oracle_loop(unet_fn, latents, imgl, ide, aud, vas, pose, added, masks, gate, N, fpb, steps):
+    """oracle.denoise_loop truncated to `steps` sampler steps (same schedule)."""
+    sig, ts = ref.euler_karras_tables(25)
+    T = N + fpb
+    lat = latents.clone()
+    shift = 0
+    for i in range(steps):
+        pred = torch.zeros_like(lat)
+        cnt = torch.zeros(1, T, 1, 1, 1)
+        for index_start in range(0, T, fpb):
+            s0 = index_start - shift
+            idx = [(j % T) for j in range(s0, s0 + fpb)]
+            x = torch.cat([lat[:, idx]] * 4) / ((sig[i] ** 2 + 1) ** 0.5)
+            x = torch.cat([x, imgl[:, idx]], dim=2)
+            ehs = (ide[:, idx].flatten(0, 1), [aud[:, idx].flatten(0, 1) * gate[0], vas[:, idx].flatten(0, 1) * gate[1]])
+            noise = unet_fn(x, ts[i], ehs, added, pose[:, idx].repeat(4, 1, 1, 1, 1), {"ip_adapter_masks": masks})
+            u, dav, dv, c = noise.chunk(4)
+            eps = u + 2.0 * (dav - u) + 7.5 * (dv - dav) + 3.0 * (c - dv)
+            out = ref.euler_step_v(eps, sig[i], sig[i + 1], lat[:, idx])
+            for j in range(fpb):
+                pred[:, (s0 + j) % T] += out[:, j]
+                cnt[:, (s0 + j) % T] += 1
+        shift = (shift + 1) % fpb
+        lat = pred / cnt
+    return lat

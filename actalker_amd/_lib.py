@@ -113,6 +113,7 @@ class ScanDesc(ctypes.Structure):
         ("nb", c_int), ("L", c_int), ("D", c_int), ("R", c_int), ("N", c_int), ("n_keep", c_int),
         ("delta", c_vp), ("ld_delta", c_int), ("delta_f32", c_int), ("softplus", c_int),
         ("G", c_int), ("u_gstride", c_int), ("y_gstride", c_int), ("flip1", c_int),
+        ("nchunks", c_int), ("chunk_len", c_int), ("ws", c_vp),
     ]
 
 
@@ -129,6 +130,7 @@ SIGNATURES = {
     "acth_groupnorm_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
     "acth_mamba_combine_ln": ([_P(MambaCombineDesc), c_vp], c_int),
     "acth_selective_scan": ([_P(ScanDesc), c_vp], c_int),
+    "acth_selective_scan_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
     "acth_timestep_embedding": ([c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_vp, c_vp], c_int),
     "acth_nchw_to_tokens": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "acth_tokens_to_nchw": ([c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),

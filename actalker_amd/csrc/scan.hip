@@ -10,34 +10,56 @@
 // direction 1 visits l = L-1..0, i.e. the reference's flip_L(x) copy becomes a traversal order;
 // outputs kept for l < n_keep (selected image tokens; ID / condition tokens only feed the state).
 //
+// Parallelism. One thread owns one (b, k, d) recurrence; at ACTalker's level-0 shape that is only
+// 56*2*640 = 71,680 sequences (~1 wave per SIMD) of 9,249 serial steps, so the sequence is split
+// into nchunks chunks scanned in two passes:
+//   pass 1: every chunk but the last scans from h = 0 and records its end state H_c and sum(delta)_c;
+//   pass 2: chunk c folds h_in = sum_j<c ( prod_{j<i<c} exp(A*Sdelta_i) ) H_j (exact recurrence
+//           composition, 16 FMAs + exps per earlier chunk) and rescans, writing y.
+// Work is ~1.8x one pass, but nchunks x more waves hide the per-token latency.
+//
 // Layout: u / delta / y token-major (b*L + l, channels): a wave reads 64 consecutive channels of one
-// token (coalesced 128 B). xdbl rows (dt | B | C, fp32) are wave-uniform per token: staged in LDS
-// per chunk of T tokens and read back as broadcasts. The next chunk's tiles are prefetched into
-// registers while the current chunk is scanned. State and exp(A) constants live in registers.
+// token (coalesced). xdbl rows (dt | B | C, fp32) are wave-uniform per token: staged in LDS per
+// tile of SC_T tokens, read back as broadcasts; the next tile is prefetched into registers while
+// the current one is scanned. State and exp(A) constants stay in registers.
 #include "common.h"
 
 #define SC_T 16
 #define SC_THREADS 128
-#define SC_WMAX 128   // max R + 2N floats per token and group
 
-template <int RMAX>
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ float softplus_fast(float x) {
+  // log1p(exp(x)) = max(x, 0) + log1p(exp(-|x|)); torch's threshold (x > 20 -> x) is implied
+  const float e = fast_exp2(-fabsf(x) * 1.4426950408889634f);
+  return fmaxf(x, 0.0f) + __logf(1.0f + e);
+}
+
+// R: dt rank (compile-time, 0 = explicit delta input). PASS: 0 single pass, 1 chunk state, 2 chunk output.
+template <int R, int PASS>
 __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) {
-  __shared__ __attribute__((aligned(16))) float xs[SC_T * SC_WMAX];
+  constexpr int W = R + 32;                      // floats per token and group in xdbl
+  constexpr int WP = (W + 3) & ~3;               // LDS row (16-byte aligned)
+  constexpr int NX = (SC_T * W + SC_THREADS - 1) / SC_THREADS;
+  __shared__ __attribute__((aligned(16))) float xs[SC_T * WP];
   __shared__ __attribute__((aligned(16))) bf16_t us[SC_T * SC_THREADS];
-  __shared__ __attribute__((aligned(16))) float dls[SC_T * SC_THREADS];
-  const int k = blockIdx.y, b = blockIdx.z;
+  __shared__ __attribute__((aligned(16))) float dls[R == 0 ? SC_T * SC_THREADS : 4];
+
+  const int k = blockIdx.y;
+  const int nc = p.nchunks;
+  const int c = blockIdx.z % nc, b = blockIdx.z / nc;
   const int t = threadIdx.x;
   const int dbase = blockIdx.x * SC_THREADS;
   const int d = dbase + t;
   const bool active = d < p.D;
   const int dd = active ? d : 0;
-  const int W = p.R + 32;
-  const bool has_delta = p.delta != nullptr;
   const bool rev = (k == 1) && p.flip1;
+  const int i_begin = c * p.chunk_len;
+  const int i_end = min(p.L, i_begin + p.chunk_len);
 
-  float w[RMAX];
+  float w[R > 0 ? R : 1];
 #pragma unroll
-  for (int r = 0; r < RMAX; ++r) w[r] = r < p.R ? p.dt_w[((size_t)k * p.D + dd) * p.R + r] : 0.0f;
+  for (int r = 0; r < R; ++r) w[r] = p.dt_w[((size_t)k * p.D + dd) * R + r];
   const float bias = p.dt_b ? p.dt_b[k * p.D + dd] : 0.0f;
   float a2[16], h[16];
 #pragma unroll
@@ -47,54 +69,60 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
   }
   const float dsk = p.Dskip ? p.Dskip[k * p.D + dd] : 0.0f;
 
+  // chunk workspace: [(b*G + k)*nc + c][17][D]  (H[0..15], sum delta)
+  float* wsb = p.ws + (((size_t)b * p.G + k) * nc) * 17 * (size_t)p.D + dd;
+  if (PASS == 2) {
+    for (int j = 0; j < c; ++j) {
+      const float* src = wsb + (size_t)j * 17 * p.D;
+      const float sd = src[16 * (size_t)p.D];
+#pragma unroll
+      for (int n = 0; n < 16; ++n) h[n] = fmaf(fast_exp2(a2[n] * sd), h[n], src[(size_t)n * p.D]);
+    }
+  }
+
   const bf16_t* ub = (const bf16_t*)p.u + (size_t)b * p.L * p.ldu + (size_t)k * p.u_gstride + dbase;
   const float* xb = p.xdbl + (size_t)b * p.L * p.ldx + k * W;
   const size_t dl_off = (size_t)b * p.L * p.ld_delta + (size_t)k * p.D + dbase;
   bf16_t* yb = (p.y1 && k == 1) ? (bf16_t*)p.y1 : (bf16_t*)p.y0 + (size_t)k * p.y_gstride;
   yb += (size_t)b * p.n_keep * p.ldy + dd;
 
-  const int nchunks = (p.L + SC_T - 1) / SC_T;
-  const int per_thread = (SC_T * W + SC_THREADS - 1) / SC_THREADS;
-
-  float px[(SC_T * SC_WMAX) / SC_THREADS];
+  float px[NX];
   uint4 pu[2];
-  float4 pd[4];
+  float4 pd[R == 0 ? 4 : 1];
 
   auto pos_of = [&](int i) { return rev ? p.L - 1 - i : i; };
-  auto prefetch = [&](int c) {
+  auto prefetch = [&](int i0) {
 #pragma unroll
-    for (int e = 0; e < (SC_T * SC_WMAX) / SC_THREADS; ++e) {
-      if (e < per_thread) {
-        const int idx = t + e * SC_THREADS;
-        const int tt = idx / W, col = idx - tt * W;
-        const int i = c * SC_T + tt;
-        px[e] = (tt < SC_T && i < p.L) ? xb[(size_t)pos_of(i) * p.ldx + col] : 0.0f;
-      }
+    for (int e = 0; e < NX; ++e) {
+      const int idx = t + e * SC_THREADS;
+      const int tt = idx / W, col = idx - tt * W;
+      const int i = i0 + tt;
+      px[e] = (tt < SC_T && i < i_end) ? xb[(size_t)pos_of(i) * p.ldx + col] : 0.0f;
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int idx = t + e * SC_THREADS;          // 256 x 16 B = 16 tokens x 128 channels
       const int tt = idx >> 4, cc = (idx & 15) * 8;
-      const int i = c * SC_T + tt;
-      pu[e] = (i < p.L && dbase + cc < p.D)
+      const int i = i0 + tt;
+      pu[e] = (i < i_end && dbase + cc < p.D)
                   ? *reinterpret_cast<const uint4*>(ub + (size_t)pos_of(i) * p.ldu + cc)
                   : make_uint4(0, 0, 0, 0);
     }
-    if (has_delta) {
+    if constexpr (R == 0) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int idx = t + e * SC_THREADS;        // 512 x 4 floats = 16 tokens x 128 channels
         const int tt = idx >> 5, cc = (idx & 31) * 4;
-        const int i = c * SC_T + tt;
+        const int i = i0 + tt;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i < p.L && dbase + cc < p.D) {
+        if (i < i_end && dbase + cc < p.D) {
           const size_t o = dl_off + (size_t)pos_of(i) * p.ld_delta + cc;
           if (p.delta_f32) {
             v = *reinterpret_cast<const float4*>((const float*)p.delta + o);
           } else {
-            const uint2 r = *reinterpret_cast<const uint2*>((const bf16_t*)p.delta + o);
-            v = make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
-                            __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u));
+            const uint2 r2 = *reinterpret_cast<const uint2*>((const bf16_t*)p.delta + o);
+            v = make_float4(__uint_as_float(r2.x << 16), __uint_as_float(r2.x & 0xffff0000u),
+                            __uint_as_float(r2.y << 16), __uint_as_float(r2.y & 0xffff0000u));
           }
         }
         pd[e] = v;
@@ -103,18 +131,16 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
   };
   auto commit = [&]() {
 #pragma unroll
-    for (int e = 0; e < (SC_T * SC_WMAX) / SC_THREADS; ++e) {
-      if (e < per_thread) {
-        const int idx = t + e * SC_THREADS;
-        if (idx < SC_T * W) xs[(idx / W) * SC_WMAX + (idx % W)] = px[e];
-      }
+    for (int e = 0; e < NX; ++e) {
+      const int idx = t + e * SC_THREADS;
+      if (idx < SC_T * W) xs[(idx / W) * WP + (idx % W)] = px[e];
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int idx = t + e * SC_THREADS;
       *reinterpret_cast<uint4*>(&us[(idx >> 4) * SC_THREADS + (idx & 15) * 8]) = pu[e];
     }
-    if (has_delta) {
+    if constexpr (R == 0) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int idx = t + e * SC_THREADS;
@@ -123,56 +149,109 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
     }
   };
 
-  prefetch(0);
-  for (int c = 0; c < nchunks; ++c) {
+  float dsum = 0.0f;
+  if (i_begin < i_end) prefetch(i_begin);
+  for (int i0 = i_begin; i0 < i_end; i0 += SC_T) {
     commit();
     __syncthreads();
-    if (c + 1 < nchunks) prefetch(c + 1);
-#pragma unroll 2
-    for (int tt = 0; tt < SC_T; ++tt) {
-      const int i = c * SC_T + tt;
-      if (i >= p.L) break;
-      const float* xr = xs + tt * SC_WMAX;
+    if (i0 + SC_T < i_end) prefetch(i0 + SC_T);
+    const int nt = min(SC_T, i_end - i0);
+    for (int tt = 0; tt < nt; ++tt) {
+      const float4* xr4 = reinterpret_cast<const float4*>(xs + tt * WP);
       float dt = bias;
-      if (has_delta) dt += dls[tt * SC_THREADS + t];
+      if constexpr (R == 0) {
+        dt += dls[tt * SC_THREADS + t];
+      } else {
 #pragma unroll
-      for (int r = 0; r < RMAX; ++r)
-        if (r < p.R) dt = fmaf(w[r], xr[r], dt);
-      if (p.softplus) dt = softplus_f(dt);
+        for (int r4 = 0; r4 < R / 4; ++r4) {
+          const float4 v = xr4[r4];
+          dt = fmaf(w[4 * r4], v.x, dt);
+          dt = fmaf(w[4 * r4 + 1], v.y, dt);
+          dt = fmaf(w[4 * r4 + 2], v.z, dt);
+          dt = fmaf(w[4 * r4 + 3], v.w, dt);
+        }
+#pragma unroll
+        for (int r = (R / 4) * 4; r < R; ++r) dt = fmaf(w[r], xs[tt * WP + r], dt);
+      }
+      if (p.softplus) dt = softplus_fast(dt);
+      if (PASS == 1) dsum += dt;
       const float uu = bf2f(us[tt * SC_THREADS + t]);
       const float du = dt * uu;
-      const float* Bv = xr + p.R;
-      const float* Cv = xr + p.R + 16;
+      const float* Bv = xs + tt * WP + R;
+      float bc[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(Bv + 4 * q);
+        bc[4 * q] = v.x; bc[4 * q + 1] = v.y; bc[4 * q + 2] = v.z; bc[4 * q + 3] = v.w;
+      }
       float y = 0.0f;
 #pragma unroll
       for (int n = 0; n < 16; ++n) {
-        h[n] = fmaf(exp2f(dt * a2[n]), h[n], du * Bv[n]);
-        y = fmaf(h[n], Cv[n], y);
+        h[n] = fmaf(fast_exp2(dt * a2[n]), h[n], du * bc[n]);
+        if (PASS != 1) y = fmaf(h[n], bc[16 + n], y);
       }
-      y = fmaf(dsk, uu, y);
-      const int l = pos_of(i);
-      if (active && l < p.n_keep) yb[(size_t)l * p.ldy] = f2bf(y);
+      if (PASS != 1) {
+        y = fmaf(dsk, uu, y);
+        const int l = pos_of(i0 + tt);
+        if (active && l < p.n_keep) yb[(size_t)l * p.ldy] = f2bf(y);
+      }
     }
     __syncthreads();
   }
+  if (PASS == 1 && active) {
+    float* dst = wsb + (size_t)c * 17 * p.D;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) dst[(size_t)n * p.D] = h[n];
+    dst[16 * (size_t)p.D] = dsum;
+  }
 }
 
-extern "C" int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream) {
-  if (!d || !d->u || !d->xdbl || !d->A_log || !d->y0) return ACTH_EINVAL;
-  if (d->R > 0 && (!d->dt_w || d->delta)) return ACTH_EINVAL;       // exactly one delta source
-  if (d->R == 0 && !d->delta) return ACTH_EINVAL;
-  if (d->N != 16 || d->R < 0 || d->R + 32 > SC_WMAX || d->L <= 0 || d->D <= 0 || d->nb <= 0) return ACTH_EINVAL;
-  if (d->G < 1 || d->G > 65535 || (d->flip1 && d->G != 2) || (d->y1 && d->G != 2)) return ACTH_EINVAL;
-  if (d->n_keep < 0 || d->n_keep > d->L || d->ldx < d->G * (d->R + 32)) return ACTH_EINVAL;
-  if (d->D % 8 || d->ldu % 8 || (d->delta && (d->D % 4 || d->ld_delta % 4))) return ACTH_EINVAL;
-  if (d->nb > 65535) return ACTH_EINVAL;
-  if (d->n_keep == 0) return ACTH_OK;
-  dim3 grid((d->D + SC_THREADS - 1) / SC_THREADS, d->G, d->nb);
-  if (d->R <= 8) hipLaunchKernelGGL(scan_kernel<8>, grid, dim3(SC_THREADS), 0, stream, *d);
-  else if (d->R <= 20) hipLaunchKernelGGL(scan_kernel<20>, grid, dim3(SC_THREADS), 0, stream, *d);
-  else if (d->R <= 40) hipLaunchKernelGGL(scan_kernel<40>, grid, dim3(SC_THREADS), 0, stream, *d);
-  else if (d->R <= 80) hipLaunchKernelGGL(scan_kernel<80>, grid, dim3(SC_THREADS), 0, stream, *d);
-  else hipLaunchKernelGGL(scan_kernel<96>, grid, dim3(SC_THREADS), 0, stream, *d);
+template <int R>
+static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
+  const unsigned gx = (d.D + SC_THREADS - 1) / SC_THREADS;
+  if (d.nchunks <= 1) {
+    hipLaunchKernelGGL((scan_kernel<R, 0>), dim3(gx, d.G, d.nb), dim3(SC_THREADS), 0, stream, d);
+  } else {
+    ActhScanDesc d1 = d;
+    // pass 1 needs every chunk but the last; launching all keeps the grid math simple
+    hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * d.nchunks), dim3(SC_THREADS), 0, stream, d1);
+    ACTH_CHECK_LAUNCH();
+    hipLaunchKernelGGL((scan_kernel<R, 2>), dim3(gx, d.G, d.nb * d.nchunks), dim3(SC_THREADS), 0, stream, d);
+  }
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
+}
+
+extern "C" size_t acth_selective_scan_workspace_size(int nb, int G, int D, int nchunks) {
+  return nchunks <= 1 ? 0 : (size_t)nb * G * nchunks * 17 * (size_t)D * sizeof(float);
+}
+
+extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
+  if (!dp) return ACTH_EINVAL;
+  ActhScanDesc d = *dp;
+  if (!d.u || !d.xdbl || !d.A_log || !d.y0) return ACTH_EINVAL;
+  if (d.R > 0 && (!d.dt_w || d.delta)) return ACTH_EINVAL;          // exactly one delta source
+  if (d.R == 0 && !d.delta) return ACTH_EINVAL;
+  if (d.N != 16 || d.R < 0 || d.L <= 0 || d.D <= 0 || d.nb <= 0) return ACTH_EINVAL;
+  if (d.G < 1 || d.G > 65535 || (d.flip1 && d.G != 2) || (d.y1 && d.G != 2)) return ACTH_EINVAL;
+  if (d.n_keep < 0 || d.n_keep > d.L || d.ldx < d.G * (d.R + 32)) return ACTH_EINVAL;
+  if (d.D % 8 || d.ldu % 8 || (d.delta && (d.D % 4 || d.ld_delta % 4))) return ACTH_EINVAL;
+  if (d.n_keep == 0) return ACTH_OK;
+  if (d.nchunks < 1) d.nchunks = 1;
+  if (d.nchunks > d.L) d.nchunks = d.L;
+  d.chunk_len = (d.L + d.nchunks - 1) / d.nchunks;
+  d.chunk_len = (d.chunk_len + SC_T - 1) / SC_T * SC_T;
+  d.nchunks = (d.L + d.chunk_len - 1) / d.chunk_len;
+  if (d.nchunks > 1 && !d.ws) return ACTH_EINVAL;
+  if ((long long)d.nb * d.nchunks > 65535) return ACTH_EINVAL;
+  switch (d.R) {
+    case 0: return launch_scan<0>(d, stream);
+    case 1: return launch_scan<1>(d, stream);
+    case 2: return launch_scan<2>(d, stream);
+    case 4: return launch_scan<4>(d, stream);
+    case 20: return launch_scan<20>(d, stream);
+    case 40: return launch_scan<40>(d, stream);
+    case 80: return launch_scan<80>(d, stream);
+    default: return ACTH_EINVAL;   // dt_rank = ceil(d_model / 16): 20/40/80 in the SVD UNet; 1,2,4 toy widths
+  }
 }

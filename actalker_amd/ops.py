@@ -286,7 +286,7 @@ def mamba_combine_ln(branch_a: dict, branch_e: dict, gamma, beta, eps: float, M:
 
 
 def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip, *, nb: int, L: int, R: int,
-                   n_keep: int, y0=None, y1=None):
+                   n_keep: int, y0=None, y1=None, nchunks: Optional[int] = None):
     """Fused bidirectional scan. u: (nb*L, D) bf16, xdbl: (nb*L, 2*(R+32)) fp32."""
     lib = _lib.load()
     _need(u, torch.bfloat16, "scan u")
@@ -309,13 +309,34 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
     d.y0, d.y1, d.ldy = y0.data_ptr(), y1.data_ptr(), _rows(y0, "scan y0")
     d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, R, 16, n_keep
     d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = 1, 2, 0, 0, 1
+    ws = _scan_chunking(d, nb, 2, D, L, nchunks, u.device)
     _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
+    del ws
     return y0, y1
+
+
+def scan_auto_chunks(nb: int, G: int, D: int, L: int, target_waves: int = 8192, min_chunk: int = 128) -> int:
+    """Chunks so that (sequences / 64) * chunks >= target_waves, chunks of >= min_chunk tokens."""
+    waves = nb * G * ((D + 63) // 64)
+    want = -(-target_waves // max(waves, 1))
+    return int(max(1, min(want, L // min_chunk)))
+
+
+def _scan_chunking(d, nb, G, D, L, nchunks, device):
+    lib = _lib.load()
+    nc = scan_auto_chunks(nb, G, D, L) if nchunks is None else int(nchunks)
+    d.nchunks = nc
+    ws = None
+    if nc > 1:
+        nbytes = lib.acth_selective_scan_workspace_size(nb, G, D, nc)
+        ws = torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32)
+        d.ws = ws.data_ptr()
+    return ws
 
 
 def selective_scan_op(u_t: torch.Tensor, delta_t: torch.Tensor, bc: torch.Tensor, A_log: torch.Tensor,
                       Dskip: Optional[torch.Tensor], delta_bias: Optional[torch.Tensor], *, nb: int, L: int,
-                      G: int, softplus: bool, out: Optional[torch.Tensor] = None):
+                      G: int, softplus: bool, out: Optional[torch.Tensor] = None, nchunks: Optional[int] = None):
     """Generic op mode: u_t (nb*L, G*D) bf16, delta_t (nb*L, G*D) fp32/bf16, bc (nb*L, G*32) fp32
     [B(16) | C(16)] per group, forward traversal, all L outputs -> (nb*L, G*D) bf16."""
     lib = _lib.load()
@@ -336,7 +357,9 @@ def selective_scan_op(u_t: torch.Tensor, delta_t: torch.Tensor, bc: torch.Tensor
     d.delta, d.ld_delta = delta_t.data_ptr(), _rows(delta_t, "scan delta")
     d.delta_f32 = int(delta_t.dtype == torch.float32)
     d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = int(softplus), G, D, D, 0
+    ws = _scan_chunking(d, nb, G, D, L, nchunks, u_t.device)
     _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
+    del ws
     return out
 
 

@@ -74,9 +74,22 @@ def unit_owner(n_windows: int, world: int, n_branch: int = 4) -> List[Tuple[int,
     return owners
 
 
+def gate_masks(gate, face_mask: torch.Tensor, mouth_mask: torch.Tensor, exp_mask: torch.Tensor):
+    """ip_adapter_masks for a gate (pipeline:702-711): [1,1] -> [mouth, exp]; [1,0] -> [face, 0];
+    [0,1] -> [0, face]."""
+    if gate[0] == 1 and gate[1] == 1:
+        return [mouth_mask, exp_mask]
+    if gate[0] == 1 and gate[1] == 0:
+        return [face_mask, torch.zeros_like(face_mask)]
+    if gate[0] == 0 and gate[1] == 1:
+        return [torch.zeros_like(face_mask), face_mask]
+    raise ValueError(f"unsupported gate {gate}")
+
+
 # ------------------------------------------------------------------------------------------ backend
 class HipBackend:
-    """Runs units through the HIP UNet (forward_tokens) and the fused guidance/Euler kernel."""
+    """Runs units through the HIP UNet (forward_tokens) and the fused guidance/Euler kernel.
+    ``masks`` = (face_mask, mouth_mask, exp_mask), each (1, 1, H_px, W_px) (pipeline:636-646)."""
 
     def __init__(self, unet, H: int, W: int, masks, gate, added_time_ids: torch.Tensor, T: int, fpb: int,
                  image_latents, image_embeddings, audio_prompts, vasa_prompts, pose_fea):
@@ -87,7 +100,7 @@ class HipBackend:
         self.dev = dev
         self.H, self.W, self.S = H, W, H * W
         self.T, self.F = T, fpb
-        self.masks = masks
+        self.masks = gate_masks(gate, *masks)
         self.gate = list(gate)
         nb = image_latents.shape[0]
         # conditioning in device layouts, converted once per run

@@ -80,7 +80,9 @@ def synthetic_inputs(N, fpb, H, W, mode, seed=72589):
     latents = 0.18215 * ref_lat[:, None] + sigma0 * noise                 # scheduler.add_noise at t0
     added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
     ones = torch.ones(1, 1, H, W)
-    masks = [ones, ones]                                                 # face mask = all ones (no face model)
+    # (face, mouth, exp): without face models preprocessing falls back to a full-image face mask, and
+    # Inference.py:545-546 overwrites the mouth / expression masks with ones
+    masks = (ones, ones, ones)
     return dict(latents=latents, image_latents=imgl.contiguous(), image_embeddings=ide.contiguous(),
                 audio_prompts=aud.contiguous(), vasa_prompts=vas.contiguous(), pose_fea=pose, added=added,
                 masks=masks)

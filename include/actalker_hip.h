@@ -138,8 +138,12 @@ typedef struct ActhScanDesc {
   int nb, L, D, R, N, n_keep;
   const void* delta; int ld_delta; int delta_f32; int softplus;
   int G, u_gstride, y_gstride, flip1;
+  int nchunks;                /* >1: two-pass chunked scan (needs ws); 0/1: single pass */
+  int chunk_len;              /* derived by the library (ignored on input) */
+  float* ws;                  /* acth_selective_scan_workspace_size(nb, G, D, nchunks) bytes */
 } ActhScanDesc;
 int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream);
+size_t acth_selective_scan_workspace_size(int nb, int G, int D, int nchunks);
 
 /* ---- small kernels */
 int acth_timestep_embedding(const float* t, int n, int dim, int flip_sin_to_cos, float downscale_freq_shift,

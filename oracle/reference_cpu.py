@@ -457,12 +457,13 @@ def denoise_loop(unet_fn, latents_all, image_latents, image_embeddings, audio_pr
             ide = image_embeddings[:, idx_list]
             aud = audio_prompts[:, idx_list]
             vas = vasa_prompts[:, idx_list]
+            face_mask, mouth_mask, exp_mask = masks          # pipeline:636-646, 702-711
             if gate[0] == 1 and gate[1] == 1:
-                mask_list = [masks[0], masks[1]]
+                mask_list = [mouth_mask, exp_mask]
             elif gate[0] == 1 and gate[1] == 0:
-                mask_list = [masks[0], torch.zeros_like(masks[0])]
+                mask_list = [face_mask, torch.zeros_like(face_mask)]
             else:
-                mask_list = [torch.zeros_like(masks[0]), masks[0]]
+                mask_list = [torch.zeros_like(face_mask), face_mask]
             sigma = sigmas[i]
             inp = torch.cat([lat] * 4) / ((sigma ** 2 + 1) ** 0.5)
             inp = torch.cat([inp, img], dim=2)

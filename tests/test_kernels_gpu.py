@@ -236,14 +236,15 @@ def _scan_case(nb, L, D, R, n_keep, g):
     return u, xproj, dtw, dtb, alog, Dp
 
 
-@pytest.mark.parametrize("nb,L,D,R,n_keep", [(2, 40, 64, 4, 30), (1, 300, 640, 20, 267), (2, 97, 1280, 40, 64),
-                                             (1, 33, 2560, 80, 0), (3, 17, 128, 80, 17)])
-def test_selective_scan_fused(dev, nb, L, D, R, n_keep):
+@pytest.mark.parametrize("nb,L,D,R,n_keep,nchunks", [
+    (2, 40, 64, 4, 30, 1), (2, 40, 64, 4, 30, 3), (1, 300, 640, 20, 267, 1), (1, 300, 640, 20, 267, 5),
+    (2, 97, 1280, 40, 64, 2), (1, 33, 2560, 80, 0, None), (3, 17, 128, 80, 17, 2), (1, 1000, 128, 20, 968, None)])
+def test_selective_scan_fused(dev, nb, L, D, R, n_keep, nchunks):
     g = torch.Generator().manual_seed(nb * 1000 + L)
     u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
     xdbl = u.float() @ bf(xproj).float().t()                        # (nb*L, 2*(R+32))
     y0, y1 = ops.selective_scan(u.to(dev), xdbl.to(dev), dtw.to(dev), dtb.to(dev), alog.to(dev), Dp.to(dev),
-                                nb=nb, L=L, R=R, n_keep=n_keep)
+                                nb=nb, L=L, R=R, n_keep=n_keep, nchunks=nchunks)
     if n_keep == 0:
         return
     # oracle: reference layout (SS2D_Unit.forward_core + selective_scan_ref)

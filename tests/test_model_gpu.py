@@ -108,7 +108,9 @@ def test_pipeline_loop_matches_oracle(dev, tiny):
     vas = torch.randn(4, T, 1, 1024, generator=g)
     pose = 0.1 * torch.randn(1, T, 64, H, W, generator=g)
     added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
-    masks = [torch.ones(1, 1, 8 * H, 8 * W), torch.ones(1, 1, 8 * H, 8 * W)]
+    lower = torch.zeros(1, 1, 8 * H, 8 * W)
+    lower[..., 4 * H:, :] = 1.0
+    masks = (torch.ones(1, 1, 8 * H, 8 * W), lower, 1 - lower)     # face, mouth, expression
     gate = [1, 1]
     lc = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, num_inference_steps=25)
     backend = pl.HipBackend(unet, H, W, masks, gate, added, T, fpb, imgl, ide, aud, vas, pose)
@@ -139,7 +141,10 @@ def _oracle_loop(unet_fn, latents, imgl, ide, aud, vas, pose, added, masks, gate
             x = torch.cat([lat[:, idx]] * 4) / ((sig[i] ** 2 + 1) ** 0.5)
             x = torch.cat([x, imgl[:, idx]], dim=2)
             ehs = (ide[:, idx].flatten(0, 1), [aud[:, idx].flatten(0, 1) * gate[0], vas[:, idx].flatten(0, 1) * gate[1]])
-            noise = unet_fn(x, ts[i], ehs, added, pose[:, idx].repeat(4, 1, 1, 1, 1), {"ip_adapter_masks": masks})
+            face, mouth, expm = masks                        # pipeline:702-711
+            mlist = ([mouth, expm] if gate == [1, 1] else [face, torch.zeros_like(face)] if gate == [1, 0]
+                     else [torch.zeros_like(face), face])
+            noise = unet_fn(x, ts[i], ehs, added, pose[:, idx].repeat(4, 1, 1, 1, 1), {"ip_adapter_masks": mlist})
             u, dav, dv, c = noise.chunk(4)
             eps = u + 2.0 * (dav - u) + 7.5 * (dv - dav) + 3.0 * (c - dv)
             out = ref.euler_step_v(eps, sig[i], sig[i + 1], lat[:, idx])

@@ -248,7 +248,12 @@ extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
     case 0: return launch_scan<0>(d, stream);
     case 1: return launch_scan<1>(d, stream);
     case 2: return launch_scan<2>(d, stream);
+    case 3: return launch_scan<3>(d, stream);
     case 4: return launch_scan<4>(d, stream);
+    case 5: return launch_scan<5>(d, stream);
+    case 6: return launch_scan<6>(d, stream);
+    case 8: return launch_scan<8>(d, stream);
+    case 16: return launch_scan<16>(d, stream);
     case 20: return launch_scan<20>(d, stream);
     case 40: return launch_scan<40>(d, stream);
     case 80: return launch_scan<80>(d, stream);

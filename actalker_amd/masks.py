@@ -9,6 +9,7 @@ are evaluated once on the host in fp32 and uploaded as small index / weight arra
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Dict, Tuple
 
 import torch
@@ -51,20 +52,25 @@ class MaskInfo:
         self.pos = pos.to(device)
 
 
-_CACHE: Dict[Tuple, MaskInfo] = {}
+# keyed by the mask tensor object itself (weakly): an entry dies with its tensor, so a new mask
+# allocated at a recycled address can never hit a stale entry; in-place edits bump _version
+_CACHE: "weakref.WeakKeyDictionary[torch.Tensor, Tuple[int, Dict]]" = weakref.WeakKeyDictionary()
 
 
 def mask_info(mask: torch.Tensor, S: int, device) -> MaskInfo:
     """mask: (1, 1, H, W) (the pipeline's ``ip_adapter_masks`` entries)."""
-    key = (mask.data_ptr(), getattr(mask, "_version", 0), tuple(mask.shape), str(mask.device), S, str(device))
-    hit = _CACHE.get(key)
+    version = getattr(mask, "_version", 0)
+    ent = _CACHE.get(mask)
+    if ent is None or ent[0] != version:
+        ent = (version, {})
+        _CACHE[mask] = ent
+    key = (S, str(device))
+    hit = ent[1].get(key)
     if hit is not None:
         return hit
     m = mask.detach().to("cpu", torch.float32)[:, 0]            # (1, H, W)
     weights = mask_downsample(m, 1, S, 1)                       # IP-adapter weights (float)
     sel = weights.view(-1).int().nonzero().view(-1)             # Mamba int() truncation
     info = MaskInfo(weights, sel, S, device)
-    if len(_CACHE) > 256:
-        _CACHE.clear()
-    _CACHE[key] = info
+    ent[1][key] = info
     return info

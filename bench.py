@@ -118,7 +118,8 @@ class GemmTimer:
                 M = a.shape[0]
             self.flops += 2.0 * M * N * K
             self.launches += 1
-            self.events.append((e0, e1))
+            mode = "conv" if kw.get("conv") is not None else "temporal" if kw.get("temporal") is not None else "dense"
+            self.events.append((e0, e1, (mode, M, N, K, kw.get("act", 0))))
             return out
         ops.gemm = timed
         import actalker_amd.modules as mods
@@ -130,7 +131,22 @@ class GemmTimer:
         ops.gemm = self.orig
 
     def total_ms(self):
-        return sum(a.elapsed_time(b) for a, b in self.events)
+        return sum(a.elapsed_time(b) for a, b, _ in self.events)
+
+    def shape_report(self, top=25):
+        agg = {}
+        for a, b, key in self.events:
+            ms = a.elapsed_time(b)
+            n, t = agg.get(key, (0, 0.0))
+            agg[key] = (n + 1, t + ms)
+        tot = sum(t for _, t in agg.values())
+        lines = []
+        for key, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+            mode, M, N, K, act = key
+            tf = 2.0 * M * N * K * n / (t / 1000.0) / 1e12
+            lines.append(f"{mode:8s} M={M:7d} N={N:5d} K={K:5d} act={act} n={n:4d} ms={t:8.1f} "
+                         f"({100 * t / tot:4.1f}%) {tf:7.1f} TF/s")
+        return "\n".join(lines)
 
 
 def cpu_baseline(unet, H, W, frames=2, mode=0):
@@ -232,6 +248,8 @@ def main():
     roof = None
     if timer is not None and timer.launches:
         gemm_ms = timer.total_ms()
+        if os.environ.get("ACTH_GEMM_STATS"):
+            log(timer.shape_report())
         achieved = timer.flops / (gemm_ms / 1000.0) / 1e12
         roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
                     frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=None, kernel="gemm_bf16_kernel",

@@ -54,23 +54,26 @@ class MaskInfo:
 
 # keyed by the mask tensor object itself (weakly): an entry dies with its tensor, so a new mask
 # allocated at a recycled address can never hit a stale entry; in-place edits bump _version
-_CACHE: "weakref.WeakKeyDictionary[torch.Tensor, Tuple[int, Dict]]" = weakref.WeakKeyDictionary()
+_CACHE: Dict[int, Tuple["weakref.ref", int, Dict]] = {}
 
 
 def mask_info(mask: torch.Tensor, S: int, device) -> MaskInfo:
     """mask: (1, 1, H, W) (the pipeline's ``ip_adapter_masks`` entries)."""
     version = getattr(mask, "_version", 0)
-    ent = _CACHE.get(mask)
-    if ent is None or ent[0] != version:
-        ent = (version, {})
-        _CACHE[mask] = ent
+    ent = _CACHE.get(id(mask))
+    if ent is None or ent[0]() is not mask or ent[1] != version:
+        if len(_CACHE) > 64:
+            for k in [k for k, e in _CACHE.items() if e[0]() is None]:
+                del _CACHE[k]
+        ent = (weakref.ref(mask), version, {})
+        _CACHE[id(mask)] = ent
     key = (S, str(device))
-    hit = ent[1].get(key)
+    hit = ent[2].get(key)
     if hit is not None:
         return hit
     m = mask.detach().to("cpu", torch.float32)[:, 0]            # (1, H, W)
     weights = mask_downsample(m, 1, S, 1)                       # IP-adapter weights (float)
     sel = weights.view(-1).int().nonzero().view(-1)             # Mamba int() truncation
     info = MaskInfo(weights, sel, S, device)
-    ent[1][key] = info
+    ent[2][key] = info
     return info

@@ -43,14 +43,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsig
 
 constexpr unsigned OOB = 0x80000000u;     // any offset >= num_records reads as zero
 
-// byte offset (into A or A2) of the 8-element chunk at (row m, k); sets `second` for the A2 source
+// byte offset of the 8-element chunk at (row m, k) inside its source (A, or A2 when `second`:
+// uniform over a K tile because K1 % 64 == 0 is required for two-source operands)
 __device__ __forceinline__ unsigned a_offset(const ActhGemmDesc& p, int m, const RowInfo& ri, int k0, int k,
-                                             bool& second) {
-  second = false;
+                                             bool second) {
   if (!ri.ok || k >= p.K) return OOB;
   if (p.amode == 0) {
-    if (k < p.K1) return ((unsigned)m * p.lda + k) * 2u;
-    second = true;
+    if (!second) return ((unsigned)m * p.lda + k) * 2u;
     return ((unsigned)m * p.lda2 + (k - p.K1)) * 2u;
   }
   const int tap = k0 / p.Cin;               // uniform over the K tile (Cin % 64 == 0)
@@ -73,8 +72,7 @@ __device__ __forceinline__ unsigned a_offset(const ActhGemmDesc& p, int m, const
     if (f < 0 || f >= p.F) return OOB;
     pix = (unsigned)(m + (tap - 1) * p.S);
   }
-  if (c < p.K1) return (pix * p.lda + c) * 2u;
-  second = true;
+  if (!second) return (pix * p.lda + c) * 2u;
   return (pix * p.lda2 + (c - p.K1)) * 2u;
 }
 
@@ -86,10 +84,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  // readfirstlane: the wave id is uniform, and proving it keeps the LDS-DMA destination (M0)
+  // scalar; otherwise hipcc wraps every DMA in a waterfall loop
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int tile_n = blockIdx.x * BN;
-  const int tile_m = blockIdx.y * BM;
+  // XCD-aware tile order: dispatch deals block ids round-robin over the 8 XCDs, so block b and
+  // b + 8 share an L2. Give each XCD a contiguous run of (m, n) tiles (n fastest) so the N tiles that
+  // share an A panel are read from one L2 (bijective for any grid size).
+  const int ntn = gridDim.x;
+  const int nwg = gridDim.x * gridDim.y;
+  const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int tile_n = (lin % ntn) * BN;
+  const int tile_m = (lin / ntn) * BM;
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
   const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(p.A2 ? p.A2 : p.A, p.A2 ? a2_bytes : 0u);
@@ -126,10 +134,11 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
     const int k0 = kt * BKT;
     char* sA = smem + buf * STAGE_BYTES;
     char* sB = sA + BM * BKT * 2;
+    // A2 (skip-connection half of a channel concat) holds K columns [K1, K): one source per K tile
+    const bool second = p.A2 && ((p.amode == 0 ? k0 : k0 % p.Cin) >= p.K1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = k0 + cchunk[j] * 8;
-      bool second;
       const unsigned off = a_offset(p, arow[j], ri[j], k0, k, second);
       lds_void* dst = (lds_void*)(sA + (wave * 32 + j * 8) * 128);
       if (second) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra2, dst, 16, off, 0, 0, 0);
@@ -297,7 +306,7 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   if (!d || !d->A || !d->B || !d->C) return ACTH_EINVAL;
   if (d->M < 0 || d->N <= 0 || d->K <= 0) return ACTH_EINVAL;
   if (d->M == 0) return ACTH_OK;
-  if (d->K % 8 || d->lda % 8 || (d->A2 && (d->lda2 % 8 || d->K1 % 8)) || d->ldb % 8) return ACTH_EINVAL;
+  if (d->K % 8 || d->lda % 8 || (d->A2 && (d->lda2 % 8 || d->K1 % 64)) || d->ldb % 8) return ACTH_EINVAL;
   // 16-byte epilogue vectors need 16-byte aligned rows in C / R / MIX; otherwise scalar path
   const int esz = d->out_f32 ? 4 : 2;
   const int vec_ok = ((size_t)d->C % 16 == 0) && ((d->ldc * esz) % 16 == 0) &&

@@ -36,6 +36,7 @@ class GemmDesc(ctypes.Structure):
         ("out_f32", c_int),
         ("C", c_vp), ("ldc", c_int),
         ("orow_div", c_int), ("orow_stride", c_int), ("orow_off", c_int),
+        ("tile", c_int),
     ]
 
 

@@ -22,7 +22,7 @@
 // while the current one feeds the MFMAs. The epilogue transposes the accumulators through LDS so
 // every thread owns 8 consecutive columns of a row: bias / residual / mix loads and the output
 // store are 16-byte and fully coalesced.
-#include "common.h"
+#include "gemm_common.h"
 
 #define BM 128
 #define BN 128
@@ -31,52 +31,8 @@
 #define EPI_LD 132                            // fp32 row stride of the epilogue tile
 #define SMEM_BYTES (BM * EPI_LD * 4)          // >= 2 * STAGE_BYTES
 
-typedef __attribute__((address_space(3))) void lds_void;
 
-namespace {
-
-struct RowInfo { int b, y, x; bool ok; };
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-
-constexpr unsigned OOB = 0x80000000u;     // any offset >= num_records reads as zero
-
-// byte offset of the 8-element chunk at (row m, k) inside its source (A, or A2 when `second`:
-// uniform over a K tile because K1 % 64 == 0 is required for two-source operands)
-__device__ __forceinline__ unsigned a_offset(const ActhGemmDesc& p, int m, const RowInfo& ri, int k0, int k,
-                                             bool second) {
-  if (!ri.ok || k >= p.K) return OOB;
-  if (p.amode == 0) {
-    if (!second) return ((unsigned)m * p.lda + k) * 2u;
-    return ((unsigned)m * p.lda2 + (k - p.K1)) * 2u;
-  }
-  const int tap = k0 / p.Cin;               // uniform over the K tile (Cin % 64 == 0)
-  const int c = k - tap * p.Cin;
-  unsigned pix;
-  if (p.amode == 1) {
-    const int ky = tap / 3, kx = tap - ky * 3;
-    int iy, ix;
-    if (p.upsample) {
-      iy = ri.y + ky - 1; ix = ri.x + kx - 1;
-      if (iy < 0 || ix < 0 || iy >= 2 * p.H || ix >= 2 * p.W) return OOB;
-      iy >>= 1; ix >>= 1;
-    } else {
-      iy = ri.y * p.conv_stride + ky - 1; ix = ri.x * p.conv_stride + kx - 1;
-      if (iy < 0 || ix < 0 || iy >= p.H || ix >= p.W) return OOB;
-    }
-    pix = ((unsigned)ri.b * p.H + iy) * p.W + ix;
-  } else {
-    const int f = ri.y + tap - 1;             // ri.y holds the frame index
-    if (f < 0 || f >= p.F) return OOB;
-    pix = (unsigned)(m + (tap - 1) * p.S);
-  }
-  if (!second) return (pix * p.lda + c) * 2u;
-  return (pix * p.lda2 + (c - p.K1)) * 2u;
-}
-
-}  // namespace
+using namespace gemm;
 
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p, unsigned a_bytes,
                                                            unsigned a2_bytes, unsigned b_bytes, int vec_ok) {
@@ -114,18 +70,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
     cchunk[j] = pchunk ^ (r & 7);            // logical K chunk this lane fetches
     arow[j] = tile_m + r;
     brow[j] = tile_n + r;
-    const int m = arow[j];
-    ri[j].ok = m < p.M;
-    ri[j].b = 0; ri[j].y = 0; ri[j].x = 0;
-    if (p.amode == 1) {
-      const int hw = p.Ho * p.Wo;
-      ri[j].b = m / hw;
-      const int rem = m - ri[j].b * hw;
-      ri[j].y = rem / p.Wo;
-      ri[j].x = rem - ri[j].y * p.Wo;
-    } else if (p.amode == 2) {
-      ri[j].y = (m / p.S) % p.F;
-    }
+    ri[j] = row_info(p, arow[j]);
   }
 
   const int nk = (p.K + BKT - 1) / BKT;
@@ -135,7 +80,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
     char* sA = smem + buf * STAGE_BYTES;
     char* sB = sA + BM * BKT * 2;
     // A2 (skip-connection half of a channel concat) holds K columns [K1, K): one source per K tile
-    const bool second = p.A2 && ((p.amode == 0 ? k0 : k0 % p.Cin) >= p.K1);
+    const bool second = second_source(p, k0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = k0 + cchunk[j] * 8;
@@ -209,97 +154,42 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
   for (int r0 = tid / tpr; r0 < BM; r0 += rows_per_pass) {
     const int row = tile_m + r0;
     if (row >= p.M) break;
-    const size_t prow = (size_t)(row / p.orow_div) * p.orow_stride + (row % p.orow_div) + p.orow_off;
-    float v[8];
-    int ocol;
     if (geglu) {
       // output columns [tile_n/2 + 8cg, +8): hidden at tile col 64g + j, gate at 64g + 32 + j
-      const int oc = cg * 8;                       // 0..63 within the tile's 64 output columns
-      const int g = oc >> 5, j0 = oc & 31;
-      const int hc = 64 * g + j0, gc = hc + 32;
-      ocol = tile_n / 2 + oc;
-      if (tile_n + gc >= p.N) continue;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float hv = et[r0 * EPI_LD + hc + e] * p.alpha + (p.bias ? p.bias[tile_n + hc + e] : 0.0f);
-        const float gv = et[r0 * EPI_LD + gc + e] * p.alpha + (p.bias ? p.bias[tile_n + gc + e] : 0.0f);
-        v[e] = hv * gelu_erf(gv);
-      }
+      const int oc = cg * 8;
+      const int hc = 64 * (oc >> 5) + (oc & 31);
+      if (tile_n + hc + 32 >= p.N) continue;
+      epilogue_geglu8(p, row, tile_n + hc, tile_n / 2 + oc, &et[r0 * EPI_LD + hc], &et[r0 * EPI_LD + hc + 32], vec_ok);
     } else {
       const int c0 = cg * 8;
-      ocol = tile_n + c0;
+      const int ocol = tile_n + c0;
       if (ocol >= p.N) continue;
-      const bool full = vec_ok && ocol + 8 <= p.N;
+      float v[8];
       const float4 x0 = *reinterpret_cast<const float4*>(&et[r0 * EPI_LD + c0]);
       const float4 x1 = *reinterpret_cast<const float4*>(&et[r0 * EPI_LD + c0 + 4]);
       v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
-      if (p.bias) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (ocol + e < p.N) ? p.bias[ocol + e] : 0.0f;
-      }
-      if (p.rowbias) {
-        const float* rb2 = p.rowbias + (size_t)(row / p.rb_div) * p.ldrb + ocol;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (ocol + e < p.N) ? rb2[e] : 0.0f;
-      }
-      if (p.R) {
-        size_t rrow = row;
-        if (p.rmap) rrow = (size_t)p.rmap[(row / p.r_div) % p.r_mod] * p.r_div + (row % p.r_div);
-        const bf16_t* rp = (const bf16_t*)p.R + rrow * p.ldr + ocol;
-        float t[8];
-        if (full) {
-          unpack8(*reinterpret_cast<const uint4*>(rp), t);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) t[e] = (ocol + e < p.N) ? bf2f(rp[e]) : 0.0f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += t[e];
-      }
-      if (p.act == 1) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
-      } else if (p.act == 3) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
-      }
-      if (p.MIX) {
-        const bf16_t* mp = (const bf16_t*)p.MIX + (size_t)row * p.ldmix + ocol;
-        float t[8];
-        if (full) {
-          unpack8(*reinterpret_cast<const uint4*>(mp), t);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) t[e] = (ocol + e < p.N) ? bf2f(mp[e]) : 0.0f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = p.mix_alpha * t[e] + (1.0f - p.mix_alpha) * v[e];
-      }
-      if (!full) {
-        for (int e = 0; e < 8 && ocol + e < p.N; ++e) {
-          if (p.out_f32) ((float*)p.C)[prow * p.ldc + ocol + e] = v[e];
-          else ((bf16_t*)p.C)[prow * p.ldc + ocol + e] = f2bf(v[e]);
-        }
-        continue;
-      }
-    }
-    if (!vec_ok) {
-      for (int e = 0; e < 8; ++e) {
-        if (p.out_f32) ((float*)p.C)[prow * p.ldc + ocol + e] = v[e];
-        else ((bf16_t*)p.C)[prow * p.ldc + ocol + e] = f2bf(v[e]);
-      }
-      continue;
-    }
-    if (p.out_f32) {
-      float* cp = (float*)p.C + prow * p.ldc + ocol;
-      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-      *reinterpret_cast<uint4*>((bf16_t*)p.C + prow * p.ldc + ocol) = pack8(v);
+      epilogue8(p, row, ocol, v, vec_ok);
     }
   }
+}
+
+int gemm256_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
+                   int vec_ok, hipStream_t stream);
+
+// Tile choice by a rounds x tile-area cost: 256-row tiles run one workgroup per CU (256 slots),
+// the 128x128 kernel two (512 slots) at ~2/3 of the big tiles' MFMA efficiency; between the
+// 256- and 160-column variants the one wasting fewer padded columns wins (160 divides 320/640/960).
+static int choose_tile(const ActhGemmDesc* d) {
+  if (d->tile) return d->tile & 0xff;
+  if (d->N < 128 || d->M < 256) return 1;
+  const long long mt = (d->M + 255) / 256;
+  const long long b2 = mt * ((d->N + 255) / 256), b3 = mt * ((d->N + 159) / 160);
+  const long long b1 = ((d->M + 127) / 128) * ((d->N + 127) / 128);
+  const double c2 = (double)((b2 + 255) / 256) * 65536.0;
+  const double c3 = d->act == 2 ? 1e30 : (double)((b3 + 255) / 256) * 40960.0;
+  const double c1 = (double)((b1 + 511) / 512) * 16384.0 * 1.5;
+  if (c1 < c2 && c1 < c3) return 1;
+  return c3 < c2 ? 3 : 2;
 }
 
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
@@ -328,6 +218,10 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
                                       ((d->amode == 0 ? d->K : d->Cin) - c1)) * 2 : 0;
   const long long b_bytes = ((long long)(d->N - 1) * d->ldb + d->K) * 2;
   if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) return ACTH_EINVAL;
+  const int tile = choose_tile(d) & 0xff;
+  if (tile == 2 || tile == 3)
+    return gemm256_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
+  if (tile != 1) return ACTH_EINVAL;
   dim3 grid((d->N + BN - 1) / BN, (d->M + BM - 1) / BM);
   if (grid.y > 65535) return ACTH_EINVAL;
   hipLaunchKernelGGL(gemm_bf16_kernel, grid, dim3(256), 0, stream, *d, (unsigned)a_bytes,

@@ -1,0 +1,163 @@
+// Shared pieces of the bf16 MFMA GEMM kernels (gemm.hip: 128x128 tile, gemm256.hip: 256-row tiles):
+// the implicit-conv A-operand addressing used by the LDS-DMA loaders and the fused epilogue.
+#pragma once
+#include "common.h"
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+namespace gemm {
+
+struct RowInfo { int b, y, x; bool ok; };
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+constexpr unsigned OOB = 0x80000000u;     // any offset >= num_records reads as zero
+
+// Decompose output row m into (image, y, x) for the conv loader or the frame index for the
+// temporal loader.
+__device__ __forceinline__ RowInfo row_info(const ActhGemmDesc& p, int m) {
+  RowInfo ri;
+  ri.ok = m < p.M;
+  ri.b = 0; ri.y = 0; ri.x = 0;
+  if (p.amode == 1) {
+    const int hw = p.Ho * p.Wo;
+    ri.b = m / hw;
+    const int rem = m - ri.b * hw;
+    ri.y = rem / p.Wo;
+    ri.x = rem - ri.y * p.Wo;
+  } else if (p.amode == 2) {
+    ri.y = (m / p.S) % p.F;
+  }
+  return ri;
+}
+
+// byte offset of the 8-element chunk at (row m, k) inside its source (A, or A2 when `second`:
+// uniform over a K tile because K1 % 64 == 0 is required for two-source operands)
+__device__ __forceinline__ unsigned a_offset(const ActhGemmDesc& p, int m, const RowInfo& ri, int k0, int k,
+                                             bool second) {
+  if (!ri.ok || k >= p.K) return OOB;
+  if (p.amode == 0) {
+    if (!second) return ((unsigned)m * p.lda + k) * 2u;
+    return ((unsigned)m * p.lda2 + (k - p.K1)) * 2u;
+  }
+  const int tap = k0 / p.Cin;               // uniform over the K tile (Cin % 64 == 0)
+  const int c = k - tap * p.Cin;
+  unsigned pix;
+  if (p.amode == 1) {
+    const int ky = tap / 3, kx = tap - ky * 3;
+    int iy, ix;
+    if (p.upsample) {
+      iy = ri.y + ky - 1; ix = ri.x + kx - 1;
+      if (iy < 0 || ix < 0 || iy >= 2 * p.H || ix >= 2 * p.W) return OOB;
+      iy >>= 1; ix >>= 1;
+    } else {
+      iy = ri.y * p.conv_stride + ky - 1; ix = ri.x * p.conv_stride + kx - 1;
+      if (iy < 0 || ix < 0 || iy >= p.H || ix >= p.W) return OOB;
+    }
+    pix = ((unsigned)ri.b * p.H + iy) * p.W + ix;
+  } else {
+    const int f = ri.y + tap - 1;             // ri.y holds the frame index
+    if (f < 0 || f >= p.F) return OOB;
+    pix = (unsigned)(m + (tap - 1) * p.S);
+  }
+  if (!second) return (pix * p.lda + c) * 2u;
+  return (pix * p.lda2 + (c - p.K1)) * 2u;
+}
+
+// does K tile starting at k0 read from A2 (the skip-connection half of a channel concat)?
+__device__ __forceinline__ bool second_source(const ActhGemmDesc& p, int k0) {
+  return p.A2 && ((p.amode == 0 ? k0 : k0 % p.Cin) >= p.K1);
+}
+
+__device__ __forceinline__ size_t out_row(const ActhGemmDesc& p, int row) {
+  return (size_t)(row / p.orow_div) * p.orow_stride + (row % p.orow_div) + p.orow_off;
+}
+
+__device__ __forceinline__ void store8(const ActhGemmDesc& p, size_t prow, int ocol, const float* v, bool full,
+                                       int vec_ok) {
+  if (full && vec_ok) {
+    if (p.out_f32) {
+      float* cp = (float*)p.C + prow * p.ldc + ocol;
+      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      *reinterpret_cast<uint4*>((bf16_t*)p.C + prow * p.ldc + ocol) = pack8(v);
+    }
+    return;
+  }
+  for (int e = 0; e < 8 && ocol + e < p.N; ++e) {
+    if (p.out_f32) ((float*)p.C)[prow * p.ldc + ocol + e] = v[e];
+    else ((bf16_t*)p.C)[prow * p.ldc + ocol + e] = f2bf(v[e]);
+  }
+}
+
+// Non-GEGLU epilogue of 8 consecutive output columns [ocol, ocol+8) of output row `row`;
+// v holds the raw accumulators. Applies alpha, bias, row bias, residual (row-remapped),
+// SiLU / GELU, AlphaBlender mix, and stores (16-byte vectors when aligned).
+__device__ __forceinline__ void epilogue8(const ActhGemmDesc& p, int row, int ocol, float* v, int vec_ok) {
+  const bool full = ocol + 8 <= p.N;
+  const bool vec = full && vec_ok;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+  if (p.bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += (ocol + e < p.N) ? p.bias[ocol + e] : 0.0f;
+  }
+  if (p.rowbias) {
+    const float* rb2 = p.rowbias + (size_t)(row / p.rb_div) * p.ldrb + ocol;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += (ocol + e < p.N) ? rb2[e] : 0.0f;
+  }
+  if (p.R) {
+    size_t rrow = row;
+    if (p.rmap) rrow = (size_t)p.rmap[(row / p.r_div) % p.r_mod] * p.r_div + (row % p.r_div);
+    const bf16_t* rp = (const bf16_t*)p.R + rrow * p.ldr + ocol;
+    float t[8];
+    if (vec) {
+      unpack8(*reinterpret_cast<const uint4*>(rp), t);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (ocol + e < p.N) ? bf2f(rp[e]) : 0.0f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += t[e];
+  }
+  if (p.act == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+  } else if (p.act == 3) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+  }
+  if (p.MIX) {
+    const bf16_t* mp = (const bf16_t*)p.MIX + (size_t)row * p.ldmix + ocol;
+    float t[8];
+    if (vec) {
+      unpack8(*reinterpret_cast<const uint4*>(mp), t);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (ocol + e < p.N) ? bf2f(mp[e]) : 0.0f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p.mix_alpha * t[e] + (1.0f - p.mix_alpha) * v[e];
+  }
+  store8(p, out_row(p, row), ocol, v, full, vec_ok);
+}
+
+// GEGLU epilogue: hidden h[8] at weight columns [hcol, hcol+8) and gate g[8] at hcol + 32
+// (interleaved 32-column granules); writes h * gelu(g) at output column `ocol`.
+__device__ __forceinline__ void epilogue_geglu8(const ActhGemmDesc& p, int row, int hcol, int ocol, const float* h,
+                                                const float* g, int vec_ok) {
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float hv = h[e] * p.alpha + (p.bias ? p.bias[hcol + e] : 0.0f);
+    const float gv = g[e] * p.alpha + (p.bias ? p.bias[hcol + 32 + e] : 0.0f);
+    v[e] = hv * gelu_erf(gv);
+  }
+  store8(p, out_row(p, row), ocol, v, true, vec_ok);
+}
+
+}  // namespace gemm

@@ -17,7 +17,7 @@
 
 // ------------------------------------------------------------------------------------------
 
-__global__ __launch_bounds__(256) void layernorm_kernel(const ActhLayerNormDesc p) {
+__global__ __launch_bounds__(256) void layernorm_ragged_kernel(const ActhLayerNormDesc p) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= p.M) return;
@@ -71,13 +71,115 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const ActhLayerNormDesc 
   }
 }
 
+// One row per LPR-lane group (64/LPR rows per wave), CPL 16-byte chunks per lane: every lane has
+// all of its row's loads in flight at once, which is what a 640-2560-byte row needs to approach
+// HBM bandwidth (one row per wave leaves most lanes idle and one load per lane in flight).
+template <int LPR, int CPL>
+__global__ __launch_bounds__(256) void layernorm_kernel(const ActhLayerNormDesc p) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, l = lane - sub * LPR;
+  const long long row = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / LPR) + sub;
+  const bool ok = row < p.M;
+  const long long rr = ok ? row : 0;
+  float v[CPL][8];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+    unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)p.x + rr * p.ldx + (l + LPR * i) * 8), v[i]);
+  if (p.add) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int ch = l + LPR * i;
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)p.add + (rr / p.add_div) * p.ldadd + ch * 8), a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] += a[e];
+      // round the sum to bf16 as the stored tensor will be, and normalise that value
+      const uint4 w = pack8(v[i]);
+      if (p.sum_out && ok) *reinterpret_cast<uint4*>((bf16_t*)p.sum_out + rr * p.ldsum + ch * 8) = w;
+      if (p.sum_out) unpack8(w, v[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[i][e];
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / p.C;
+  float q = 0.0f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; q += d * d; }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / p.C + p.eps);
+  if (!ok) return;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int ch = l + LPR * i;
+    float g[8], b[8], o[8];
+    if (p.gamma) {
+      const float4 g0 = reinterpret_cast<const float4*>(p.gamma + ch * 8)[0];
+      const float4 g1 = reinterpret_cast<const float4*>(p.gamma + ch * 8)[1];
+      g[0] = g0.x; g[1] = g0.y; g[2] = g0.z; g[3] = g0.w; g[4] = g1.x; g[5] = g1.y; g[6] = g1.z; g[7] = g1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = 1.0f;
+    }
+    if (p.beta) {
+      const float4 b0 = reinterpret_cast<const float4*>(p.beta + ch * 8)[0];
+      const float4 b1 = reinterpret_cast<const float4*>(p.beta + ch * 8)[1];
+      b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = 0.0f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
+    *reinterpret_cast<uint4*>((bf16_t*)p.y + row * p.ldy + ch * 8) = pack8(o);
+  }
+}
+
+template <int LPR>
+static void ln_launch(const ActhLayerNormDesc* d, int cpl, hipStream_t stream) {
+  const long long rows_per_blk = 4LL * (64 / LPR);
+  const dim3 grid((unsigned)((d->M + rows_per_blk - 1) / rows_per_blk));
+  switch (cpl) {
+    case 1: hipLaunchKernelGGL((layernorm_kernel<LPR, 1>), grid, dim3(256), 0, stream, *d); break;
+    case 2: hipLaunchKernelGGL((layernorm_kernel<LPR, 2>), grid, dim3(256), 0, stream, *d); break;
+    case 3: hipLaunchKernelGGL((layernorm_kernel<LPR, 3>), grid, dim3(256), 0, stream, *d); break;
+    case 4: hipLaunchKernelGGL((layernorm_kernel<LPR, 4>), grid, dim3(256), 0, stream, *d); break;
+    case 5: hipLaunchKernelGGL((layernorm_kernel<LPR, 5>), grid, dim3(256), 0, stream, *d); break;
+    case 6: hipLaunchKernelGGL((layernorm_kernel<LPR, 6>), grid, dim3(256), 0, stream, *d); break;
+    case 7: hipLaunchKernelGGL((layernorm_kernel<LPR, 7>), grid, dim3(256), 0, stream, *d); break;
+    default: hipLaunchKernelGGL((layernorm_kernel<LPR, 8>), grid, dim3(256), 0, stream, *d); break;
+  }
+}
+
 extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
   if (!d || !d->x || !d->y || d->C <= 0 || d->C % 8 || d->C > 64 * 8 * MAXCH) return ACTH_EINVAL;
   if (d->ldx % 8 || d->ldy % 8 || (d->add && (d->ldadd % 8 || d->add_div <= 0)) || (d->sum_out && d->ldsum % 8))
     return ACTH_EINVAL;
   if (d->M == 0) return ACTH_OK;
-  const long long nblk = ((long long)d->M + 3) / 4;
-  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  // lanes per row: the smallest of 4..64 that leaves at most 8 chunks per lane and divides the row;
+  // other widths (and unaligned gamma/beta) take the one-row-per-wave kernel
+  const int nch = d->C / 8;
+  int lpr = 0;
+  for (int c = 4; c <= 64; c *= 2)
+    if (nch % c == 0 && nch / c <= 8) { lpr = c; break; }
+  if (!lpr || ((size_t)d->gamma | (size_t)d->beta) % 16) {
+    hipLaunchKernelGGL(layernorm_ragged_kernel, dim3((unsigned)((d->M + 3) / 4)), dim3(256), 0, stream, *d);
+    ACTH_CHECK_LAUNCH();
+    return ACTH_OK;
+  }
+  const int cpl = nch / lpr;
+  if (lpr == 4) ln_launch<4>(d, cpl, stream);
+  else if (lpr == 8) ln_launch<8>(d, cpl, stream);
+  else if (lpr == 16) ln_launch<16>(d, cpl, stream);
+  else if (lpr == 32) ln_launch<32>(d, cpl, stream);
+  else ln_launch<64>(d, cpl, stream);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }
@@ -86,7 +188,14 @@ extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
 // GroupNorm. Rows are tokens; statistics batch = row / rows_per_stat; group = c / (C/G).
 // Input may be the channel concat of x (C1 channels) and x2 (C - C1 channels).
 
-#define GN_ROWS 256
+// Statistics: each block reduces GS_ROWS rows of one statistics batch to per-channel fp32 partial
+// sums (LDS), folds them to per-group sums and adds those to fp64 accumulators (2*G doubles per
+// batch). Apply: each block covers rows of a single batch, turns (mean, rstd, gamma, beta) into a
+// per-channel scale/shift once, then streams y = x * a + b (+ SiLU) with 16-byte accesses.
+// Thread layout of both: nchl = min(C/8, 256) chunk columns x (256 / nchl) row lanes; a thread
+// owns chunk columns cl and cl + nchl (C <= 4096).
+
+#define GS_ROWS 128
 
 __device__ __forceinline__ uint4 gn_load(const ActhGroupNormDesc& p, long long row, int ch) {
   const int c = ch * 8;
@@ -94,86 +203,129 @@ __device__ __forceinline__ uint4 gn_load(const ActhGroupNormDesc& p, long long r
   return *reinterpret_cast<const uint4*>((const bf16_t*)p.x2 + row * p.ldx2 + (c - p.C1));
 }
 
-// grid: (ceil(rows_per_stat / GN_ROWS), nstat)
+// grid: (ceil(rows_per_stat / GS_ROWS), nstat)
 __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p) {
+  __shared__ float red[2 * 4096];
   const int nch = p.C >> 3;
-  const int stat = blockIdx.y;
-  const long long r_begin = (long long)stat * p.rows_per_stat + (long long)blockIdx.x * GN_ROWS;
-  const long long r_end = min((long long)stat * p.rows_per_stat + p.rows_per_stat,
-                              r_begin + GN_ROWS);
-  // thread -> (chunk, row lane); when nch > 256 a thread owns chunks t, t+256, ...
-  int lanes_per_row, rows_par;
-  if (nch <= 256) { rows_par = 256 / nch; lanes_per_row = nch; }
-  else { rows_par = 1; lanes_per_row = 256; }
+  const int nchl = nch < 256 ? nch : 256;
+  const int rows_par = 256 / nchl;
   const int t = threadIdx.x;
-  if (t >= rows_par * lanes_per_row) return;
-  const int rl = t / lanes_per_row, cl = t - rl * lanes_per_row;
-  for (int ch = cl; ch < nch; ch += lanes_per_row) {
-    float s1[8], s2[8];
+  for (int c = t; c < 2 * p.C; c += 256) red[c] = 0.0f;
+  __syncthreads();
+  const int stat = blockIdx.y;
+  const long long r_begin = (long long)stat * p.rows_per_stat + (long long)blockIdx.x * GS_ROWS;
+  const long long r_end = min((long long)stat * p.rows_per_stat + p.rows_per_stat, r_begin + GS_ROWS);
+  const int rl = t / nchl, cl = t - rl * nchl;
+  if (rl < rows_par) {
+    for (int ch = cl; ch < nch; ch += nchl) {
+      float s1[8], s2[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { s1[e] = 0.0f; s2[e] = 0.0f; }
-    for (long long r = r_begin + rl; r < r_end; r += rows_par) {
-      float v[8];
-      unpack8(gn_load(p, r, ch), v);
+      for (int e = 0; e < 8; ++e) { s1[e] = 0.0f; s2[e] = 0.0f; }
+      long long r = r_begin + rl;
+      for (; r + 3 * rows_par < r_end; r += 4 * rows_par) {
+        uint4 w[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
-    }
-    double* acc = p.ws + ((size_t)stat * p.C + ch * 8) * 2;
+        for (int u = 0; u < 4; ++u) w[u] = gn_load(p, r + u * rows_par, ch);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      atomicAdd(acc + 2 * e, (double)s1[e]);
-      atomicAdd(acc + 2 * e + 1, (double)s2[e]);
+        for (int u = 0; u < 4; ++u) {
+          float v[8];
+          unpack8(w[u], v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+        }
+      }
+      for (; r < r_end; r += rows_par) {
+        float v[8];
+        unpack8(gn_load(p, r, ch), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(&red[ch * 8 + e], s1[e]);
+        atomicAdd(&red[p.C + ch * 8 + e], s2[e]);
+      }
     }
   }
-}
-
-// one thread per (stat, group): mean / rstd as floats after the per-channel double sums
-__global__ void gn_finalize_kernel(const ActhGroupNormDesc p, int nstat) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nstat * p.G) return;
-  const int stat = idx / p.G, g = idx - stat * p.G;
+  __syncthreads();
   const int cpg = p.C / p.G;
-  double s1 = 0.0, s2 = 0.0;
-  for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-    s1 += p.ws[((size_t)stat * p.C + c) * 2];
-    s2 += p.ws[((size_t)stat * p.C + c) * 2 + 1];
+  if (t < p.G) {
+    double a1 = 0.0, a2 = 0.0;
+    for (int c = t * cpg; c < (t + 1) * cpg; ++c) { a1 += red[c]; a2 += red[p.C + c]; }
+    double* acc = p.ws + ((size_t)stat * p.G + t) * 2;
+    atomicAdd(acc, a1);
+    atomicAdd(acc + 1, a2);
   }
-  const double n = (double)cpg * p.rows_per_stat;
-  const double mean = s1 / n;
-  double var = s2 / n - mean * mean;
-  if (var < 0.0) var = 0.0;
-  float* st = reinterpret_cast<float*>(p.ws + (size_t)nstat * p.C * 2);
-  st[idx * 2] = (float)mean;
-  st[idx * 2 + 1] = (float)(1.0 / sqrt(var + (double)p.eps));
 }
 
-__global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p, int nstat) {
+// grid: M / rows_per_blk blocks; every block's rows lie in one statistics batch
+__global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p, int rows_per_blk) {
   const int nch = p.C >> 3;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)p.M * nch) return;
-  const long long row = idx / nch;
-  const int ch = (int)(idx - row * nch);
-  const int stat = (int)(row / p.rows_per_stat);
+  const int nchl = nch < 256 ? nch : 256;
+  const int rows_par = 256 / nchl;
+  const int t = threadIdx.x;
+  const int rl = t / nchl, cl = t - rl * nchl;
+  if (rl >= rows_par) return;
+  const long long row0 = (long long)blockIdx.x * rows_per_blk;
+  const int stat = (int)(row0 / p.rows_per_stat);
   const int cpg = p.C / p.G;
-  const float* st = reinterpret_cast<const float*>(p.ws + (size_t)nstat * p.C * 2);
-  float v[8];
-  unpack8(gn_load(p, row, ch), v);
+  const double n = (double)cpg * p.rows_per_stat;
+  float sa[2][8], sb[2][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int c = ch * 8 + e;
-    const int g = c / cpg;
-    const float mean = st[(stat * p.G + g) * 2], rstd = st[(stat * p.G + g) * 2 + 1];
-    float o = (v[e] - mean) * rstd * p.gamma[c] + p.beta[c];
-    if (p.silu) o = silu_f(o);
-    v[e] = o;
+  for (int k = 0; k < 2; ++k) {
+    const int ch = cl + k * nchl;
+    if (ch < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = ch * 8 + e, g = c / cpg;
+        const double* acc = p.ws + ((size_t)stat * p.G + g) * 2;
+        const double mean = acc[0] / n;
+        double var = acc[1] / n - mean * mean;
+        if (var < 0.0) var = 0.0;
+        const float rstd = (float)(1.0 / sqrt(var + (double)p.eps));
+        sa[k][e] = rstd * p.gamma[c];
+        sb[k][e] = p.beta[c] - (float)mean * sa[k][e];
+      }
+    }
   }
-  *reinterpret_cast<uint4*>((bf16_t*)p.y + row * p.ldy + ch * 8) = pack8(v);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ch = cl + k * nchl;
+    if (ch >= nch) break;
+    int r = rl;
+    for (; r + 3 * rows_par < rows_per_blk; r += 4 * rows_par) {
+      uint4 w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = gn_load(p, row0 + r + u * rows_par, ch);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v[8];
+        unpack8(w[u], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float o = v[e] * sa[k][e] + sb[k][e];
+          v[e] = p.silu ? silu_f(o) : o;
+        }
+        *reinterpret_cast<uint4*>((bf16_t*)p.y + (row0 + r + u * rows_par) * p.ldy + ch * 8) = pack8(v);
+      }
+    }
+    for (; r < rows_per_blk; r += rows_par) {
+      float v[8];
+      unpack8(gn_load(p, row0 + r, ch), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float o = v[e] * sa[k][e] + sb[k][e];
+        v[e] = p.silu ? silu_f(o) : o;
+      }
+      *reinterpret_cast<uint4*>((bf16_t*)p.y + (row0 + r) * p.ldy + ch * 8) = pack8(v);
+    }
+  }
 }
 
 extern "C" size_t acth_groupnorm_workspace_size(int M, int C, int G, int rows_per_stat) {
   if (rows_per_stat <= 0) return 0;
   const size_t nstat = (size_t)M / rows_per_stat;
-  return nstat * C * 2 * sizeof(double) + nstat * G * 2 * sizeof(float);
+  return nstat * G * 2 * sizeof(double);
 }
 
 extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
@@ -181,19 +333,18 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   if (d->C % 8 || d->C1 % 8 || d->G <= 0 || d->C % d->G || d->rows_per_stat <= 0) return ACTH_EINVAL;
   if (d->M % d->rows_per_stat) return ACTH_EINVAL;
   if (d->C1 < d->C && (!d->x2 || d->ldx2 % 8)) return ACTH_EINVAL;
-  if (d->ldx % 8 || d->ldy % 8 || d->C > 8 * 512) return ACTH_EINVAL;
+  if (d->ldx % 8 || d->ldy % 8 || d->C > 4096) return ACTH_EINVAL;
   const int nstat = d->M / d->rows_per_stat;
   if (nstat == 0) return ACTH_OK;
   if (nstat > 65535) return ACTH_EINVAL;
-  if (hipMemsetAsync(d->ws, 0, (size_t)nstat * d->C * 2 * sizeof(double), stream) != hipSuccess)
+  if (hipMemsetAsync(d->ws, 0, (size_t)nstat * d->G * 2 * sizeof(double), stream) != hipSuccess)
     return ACTH_ELAUNCH;
-  dim3 g1((d->rows_per_stat + GN_ROWS - 1) / GN_ROWS, nstat);
+  dim3 g1((d->rows_per_stat + GS_ROWS - 1) / GS_ROWS, nstat);
   hipLaunchKernelGGL(gn_stats_kernel, g1, dim3(256), 0, stream, *d);
   ACTH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((nstat * d->G + 127) / 128), dim3(128), 0, stream, *d, nstat);
-  ACTH_CHECK_LAUNCH();
-  const long long n = (long long)d->M * (d->C / 8);
-  hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, *d, nstat);
+  int rpb = 128;
+  while (d->rows_per_stat % rpb) rpb >>= 1;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)(d->M / rpb)), dim3(256), 0, stream, *d, rpb);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -47,8 +47,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
          residual: Optional[torch.Tensor] = None, rmap: Optional[torch.Tensor] = None, r_div: int = 1,
          r_mod: int = 1, mix: Optional[torch.Tensor] = None, mix_alpha: float = 0.0, alpha: float = 1.0,
          act: int = ACT_NONE, out: Optional[torch.Tensor] = None, out_f32: bool = False,
-         orow: Optional[Sequence[int]] = None) -> torch.Tensor:
-    """out = epilogue(A . w^T).  ``w``: packed (N, K) bf16.
+         orow: Optional[Sequence[int]] = None, tile: int = 0) -> torch.Tensor:
+    """out = epilogue(A . w^T).  ``tile``: 0 auto, 1 128x128, 2 256x256, 3 256x160 (tests force one).  ``w``: packed (N, K) bf16.
 
     A modes: dense (a is (M, K1) [+ a2 (M, K-K1)]), ``conv=dict(H, W, Ho, Wo, stride, upsample, B)``
     (a is the NHWC image as (B*H*W, C1) [+ a2]), ``temporal=dict(F, S)`` (a is (M, C1) rows).
@@ -133,6 +133,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
             raise _lib.ActhError(f"gemm: out {tuple(out.shape)} too small for ({M}, {n_out})")
     else:
         d.orow_div, d.orow_stride, d.orow_off = orow
+    d.tile = tile
     _lib.check(lib.acth_gemm(ctypes.byref(d), _stream()), "acth_gemm")
     return out
 

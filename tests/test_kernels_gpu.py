@@ -94,6 +94,64 @@ def test_gemm_geglu_and_orow(dev):
     assert float(got[0:3].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3])
+def test_gemm_tile_variants(dev, tile):
+    """Every tile kernel (128x128; 256x256 and 256x160 8-wave) on all A loaders, tails and epilogues."""
+    from actalker_amd.modules import pack_conv3x3, pack_conv3d_t, pack_geglu
+    # dense, ragged M/N/K + bias + residual + silu, fp32 out
+    M, N, K = 700, 330, 200
+    a, w = bf(rnd(M, K)), bf(rnd(N, K, scale=K ** -0.5))
+    bias, res = rnd(N), bf(rnd(M, N))
+    out = ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), residual=res.to(dev), act=ops.ACT_SILU,
+                   out_f32=True, tile=tile)
+    assert rel(out, F.silu(a.float() @ w.float().t() + bias + res.float())) < 1e-2
+    # two-source concat + mix + rowbias
+    a2 = bf(rnd(M, 128))
+    w2 = bf(rnd(N, 192 + 128, scale=320 ** -0.5))
+    a1 = bf(rnd(M, 192))
+    rowb = rnd(2, N)
+    mix = bf(rnd(M, N))
+    out = ops.gemm(a1.to(dev), w2.to(dev), a2=a2.to(dev), rowbias=rowb.to(dev), rb_div=350, mix=mix.to(dev),
+                   mix_alpha=0.25, tile=tile)
+    base = torch.cat([a1, a2], 1).float() @ w2.float().t() + rowb.repeat_interleave(350, 0)
+    assert rel(out, 0.25 * mix.float() + 0.75 * base) < 1e-2
+    # conv3x3 with skip concat, stride 1 / 2 / upsample
+    B, H, W, C1, C2, Co = 2, 12, 20, 128, 64, 320
+    x1, x2 = bf(rnd(B, C1, H, W)), bf(rnd(B, C2, H, W))
+    wc = bf(rnd(Co, C1 + C2, 3, 3, scale=(9 * (C1 + C2)) ** -0.5))
+    tok = lambda t_: t_.permute(0, 2, 3, 1).reshape(-1, t_.shape[1]).contiguous().to(dev)
+    for mode in ("s1", "s2", "up"):
+        st = 2 if mode == "s2" else 1
+        Ho, Wo = (H * 2, W * 2) if mode == "up" else ((H - 1) // st + 1, (W - 1) // st + 1)
+        out = ops.gemm(tok(x1), pack_conv3x3(wc).to(dev), a2=tok(x2),
+                       conv=dict(H=H, W=W, Ho=Ho, Wo=Wo, stride=st, upsample=mode == "up", B=B), tile=tile)
+        xr = torch.cat([x1, x2], 1).float()
+        if mode == "up":
+            xr = F.interpolate(xr, scale_factor=2.0, mode="nearest")
+        refo = F.conv2d(xr, wc.float(), None, stride=st, padding=1)
+        assert rel(out, refo.permute(0, 2, 3, 1).reshape(-1, Co)) < 1e-2, mode
+    # temporal (3,1,1)
+    Bt, Ft, S, C, Co = 2, 7, 40, 128, 160
+    x = bf(rnd(Bt, C, Ft, 5, 8))
+    wt = bf(rnd(Co, C, 3, 1, 1, scale=(3 * C) ** -0.5))
+    tk = x.permute(0, 2, 3, 4, 1).reshape(-1, C).contiguous()
+    out = ops.gemm(tk.to(dev), pack_conv3d_t(wt).to(dev), temporal=dict(F=Ft, S=S), tile=tile)
+    refo = F.conv3d(x.float(), wt.float(), None, padding=(1, 0, 0)).permute(0, 2, 3, 4, 1).reshape(-1, Co)
+    assert rel(out, refo) < 1e-2
+    # GEGLU (the 256x160 tile rejects it: its wave tiles are not 64-column granules)
+    Mg, Cg, inner = 600, 192, 640
+    xg = bf(rnd(Mg, Cg))
+    wg, bg = rnd(2 * inner, Cg, scale=Cg ** -0.5), rnd(2 * inner, scale=0.1)
+    wp, bp = pack_geglu(wg, bg)
+    if tile == 3:
+        with pytest.raises(Exception):
+            ops.gemm(xg.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile)
+    else:
+        out = ops.gemm(xg.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile)
+        h, g = (xg.float() @ bf(wg).float().t() + bg).chunk(2, -1)
+        assert rel(out, h * F.gelu(g)) < 1e-2
+
+
 @pytest.mark.parametrize("B,H,W,C1,C2,Cout,mode", [
     (2, 9, 16, 64, 0, 128, "s1"), (3, 18, 32, 128, 64, 192, "s1"), (2, 9, 16, 128, 0, 128, "s2"),
     (2, 9, 16, 64, 0, 64, "up"), (1, 36, 64, 320, 320, 320, "s1")])

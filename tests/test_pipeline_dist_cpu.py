@@ -1,0 +1,175 @@
+"""CPU: the frame-window sharded sampler loop (actalker_amd.pipeline.denoise) over 1, 2 and 3 gloo
+ranks against the oracle's single-process loop (pipeline:670-756 semantics).
+
+The backend here is test-only and runs on the CPU: the UNet is a deterministic stand-in (a fixed
+function of the window's frames, the CFG branch and the timestep that mixes frames within the
+window), so the test isolates what the multi-GPU path adds: the (window, CFG-branch) unit
+assignment, the all-gather layout of the noise predictions and the replicated guidance + Euler +
+window accumulation. The UNet itself is parity-tested on the GPU (tests/test_model_gpu.py).
+"""
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from actalker_amd import pipeline as pl
+from oracle import reference_cpu as ref
+
+
+def fake_unet(x, branch, t):
+    """(F, 8, h, w) window input (+ branch id, timestep) -> (F, 4, h, w) 'noise'. Mixes frames with
+    a window-relative weighting so a wrong frame order or window split changes the result."""
+    F = x.shape[0]
+    w = torch.linspace(0.5, 1.5, F).view(F, 1, 1, 1)
+    mean = (x[:, :4] * w).mean(0, keepdim=True)
+    return torch.tanh(0.01 * x[:, :4] + 0.3 * x[:, 4:] + 0.05 * mean + 0.1 * (branch + 1) + 0.01 * t)
+
+
+class CpuBackend:
+    """Mirror of pipeline.HipBackend's interface on torch CPU tensors."""
+
+    def __init__(self, image_latents, h, w, T, fpb):
+        self.img = image_latents               # (4, T, 4, h, w)
+        self.h, self.w, self.S = h, w, h * w
+        self.T, self.F = T, fpb
+
+    def new_state(self, latents_all):
+        return latents_all.clone().float()     # (1, T, 4, h, w)
+
+    def run_units(self, lat, units, frames, t, sigma, out, row0):
+        F, S = self.F, self.S
+        for u, (wdx, c) in enumerate(units):
+            idx = frames[wdx]
+            x = torch.cat([lat[0, idx] / math.sqrt(sigma * sigma + 1.0), self.img[c, idx]], dim=1)
+            noise = fake_unet(x, c, t)                                        # (F, 4, h, w)
+            out[row0 + u * F * S: row0 + (u + 1) * F * S] = noise.permute(0, 2, 3, 1).reshape(-1, 4)
+
+    def step_windows(self, lat, gathered, unit_rows, frames, guidance, sigma, sigma_next):
+        F, S, h, w = self.F, self.S, self.h, self.w
+        acc = torch.zeros_like(lat)
+        cnt = torch.zeros(1, self.T, 1, 1, 1)
+        g1, g2, g3 = guidance
+        for wdx, rows in enumerate(unit_rows):
+            br = [gathered[r:r + F * S].view(F, h, w, 4).permute(0, 3, 1, 2) for r in rows]
+            u, dav, dv, c = br
+            eps = u + g1 * (dav - u) + g2 * (dv - dav) + g3 * (c - dv)
+            idx = frames[wdx]
+            out = ref.euler_step_v(eps[None], sigma, sigma_next, lat[:, idx])
+            for j, f in enumerate(idx):
+                acc[:, f] += out[:, j]
+                cnt[:, f] += 1
+        return acc / cnt
+
+    def finish(self, lat):
+        return lat
+
+
+def oracle_loop(latents, imgl, N, fpb, shift_offset, steps):
+    sig, ts = ref.euler_karras_tables(25)
+    T = N + fpb
+    lat = latents.clone()
+    shift = 0
+    for i in range(steps):
+        pred = torch.zeros_like(lat)
+        cnt = torch.zeros(1, T, 1, 1, 1)
+        for index_start in range(0, T, fpb):
+            s0 = index_start - shift
+            idx = [j % T for j in range(s0, s0 + fpb)]
+            noise = [fake_unet(torch.cat([lat[0, idx] / ((sig[i] ** 2 + 1) ** 0.5), imgl[c, idx]], 1), c, ts[i])
+                     for c in range(4)]
+            u, dav, dv, c = noise
+            eps = u + 2.0 * (dav - u) + 7.5 * (dv - dav) + 3.0 * (c - dv)
+            out = ref.euler_step_v(eps[None], sig[i], sig[i + 1], lat[:, idx])
+            for j in range(fpb):
+                pred[:, (s0 + j) % T] += out[:, j]
+                cnt[:, (s0 + j) % T] += 1
+        shift = (shift + shift_offset) % fpb
+        lat = pred / cnt
+    return lat
+
+
+def make_case(N=6, fpb=3, h=2, w=3, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    T = N + fpb
+    latents = 0.18215 * torch.randn(1, 1, 4, h, w, generator=g) + 700.0 * torch.randn(1, T, 4, h, w, generator=g)
+    imgl = torch.randn(4, T, 4, h, w, generator=g)
+    imgl[0] = 0
+    return latents, imgl
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, N, fpb, steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        latents, imgl = make_case(N, fpb)
+        backend = CpuBackend(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
+        cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1, units_per_call=2)
+        out = pl.denoise(backend, latents, cfg, rank, world, steps=steps)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unit_assignment_covers_every_unit_once():
+    for n_windows in (1, 2, 3, 9):
+        for world in (1, 2, 3, 8):
+            seen = []
+            caps = set()
+            for r in range(world):
+                units, cap = pl.assign_units(n_windows, world, r)
+                assert len(units) <= cap
+                caps.add(cap)
+                seen += units
+            assert sorted(seen) == [(w, c) for w in range(n_windows) for c in range(4)]
+            assert len(caps) == 1
+    # N = 112 -> 9 windows x 4 branches over 8 GPUs = 5,5,5,5,4,4,4,4
+    assert [len(pl.assign_units(9, 8, r)[0]) for r in range(8)] == [5, 5, 5, 5, 4, 4, 4, 4]
+
+
+def test_window_frames_wrap_and_shift():
+    assert pl.window_frames(6, 3, 0, 0) == [[0, 1, 2], [3, 4, 5]]
+    assert pl.window_frames(6, 3, 0, 1) == [[5, 0, 1], [2, 3, 4]]      # (start - shift) mod T
+
+
+def test_single_process_loop_matches_oracle():
+    N, fpb, steps = 6, 3, 4
+    latents, imgl = make_case(N, fpb)
+    backend = CpuBackend(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
+    cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1, units_per_call=2)
+    got = pl.denoise(backend, latents, cfg, steps=steps)
+    want = oracle_loop(latents, imgl, N, fpb, 1, steps)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_loop_matches_single_process(world):
+    """world ranks (gloo), contiguous unit blocks + one all-gather per step == 1 process == oracle."""
+    N, fpb, steps = 6, 3, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    latents, imgl = make_case(N, fpb)
+    want = oracle_loop(latents, imgl, N, fpb, 1, steps)
+    for r in range(world):
+        torch.testing.assert_close(outs[r], want, rtol=1e-5, atol=1e-3)
+    # every rank holds the identical latent state (replicated guidance/Euler)
+    for r in range(1, world):
+        assert torch.equal(outs[r], outs[0])

@@ -1,0 +1,74 @@
+"""Micro-benchmark of acth_gemm per tile variant on the UNet's dominant shapes (random data).
+
+  python tools/bench_gemm.py [--tiles 1,2,3] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from actalker_amd import ops  # noqa: E402
+
+# (mode, M, N, K, act) — from bench.py ACTH_GEMM_STATS at 576x1024, 56-frame calls
+SHAPES = [
+    ("dense", 516096, 2560, 320, 2), ("dense", 129024, 5120, 640, 2), ("dense", 516096, 320, 320, 0),
+    ("dense", 32256, 10240, 1280, 2), ("dense", 516096, 320, 1280, 0), ("conv", 516096, 320, 2880, 0),
+    ("dense", 129024, 640, 640, 0), ("dense", 129024, 640, 2560, 0), ("conv", 32256, 1280, 11520, 0),
+    ("temporal", 516096, 320, 960, 0), ("conv", 129024, 640, 5760, 0), ("dense", 32256, 1280, 5120, 0),
+    ("dense", 516096, 960, 320, 0), ("dense", 32256, 1280, 1280, 0), ("conv", 8064, 1280, 11520, 0),
+]
+
+
+def run(mode, M, N, K, act, tile, iters, dev):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    kw = {}
+    if mode == "conv":
+        cin = K // 9
+        H, W = (72, 128) if M == 516096 else (36, 64) if M == 129024 else (18, 32) if M == 32256 else (9, 16)
+        B = M // (H * W)
+        a = torch.randn(B * H * W, cin, generator=g).to(dev, torch.bfloat16)
+        kw["conv"] = dict(H=H, W=W, Ho=H, Wo=W, stride=1, upsample=False, B=B)
+    elif mode == "temporal":
+        cin = K // 3
+        a = torch.randn(M, cin, generator=g).to(dev, torch.bfloat16)
+        kw["temporal"] = dict(F=14, S=M // 56)
+    else:
+        a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(dev)
+    try:
+        ops.gemm(a, w, bias=bias, act=act, tile=tile, **kw)
+    except Exception as e:  # noqa: BLE001
+        return None, str(e)[:60]
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        ops.gemm(a, w, bias=bias, act=act, tile=tile, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return 2.0 * M * N * K / (ms / 1e3) / 1e12, ms
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", default="0,1,2,3")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--flags", type=int, default=0, help="OR-ed into tile (0x100: skip epilogue)")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    tiles = [int(t) for t in args.tiles.split(",")]
+    print("mode      M       N     K    act " + " ".join(f"tile{t:d}(TF/s)" for t in tiles), flush=True)
+    for (mode, M, N, K, act) in SHAPES:
+        cells = []
+        for t in tiles:
+            tf, ms = run(mode, M, N, K, act, t | args.flags, args.iters, dev)
+            cells.append(f"{tf:12.1f}" if tf is not None else f"{'n/a':>12s}")
+        print(f"{mode:8s} {M:7d} {N:5d} {K:5d} {act:3d} " + " ".join(cells), flush=True)
+
+
+if __name__ == "__main__":
+    main()

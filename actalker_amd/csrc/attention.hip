@@ -15,22 +15,41 @@
 //                        audio attention is evaluated; region masks weight it per token.
 #include "common.h"
 
+typedef __attribute__((address_space(3))) void lds_void;
+
 // ------------------------------------------------------------------------------------------
 
-#define FA_LDS 72
+// Flash attention v2 structure (per block: 4 waves x 32 queries, KV tiles of 64 keys):
+//  * K and V tiles move HBM/L2 -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows per
+//    wave-instruction), double-buffered: tile j+1 is in flight while tile j is consumed; one
+//    vmcnt(0) + barrier per tile. Rows past Skv read zeros (buffer range check).
+//  * Both tiles stay row-major [key][d] (128-B rows). K feeds S^T = K Q^T as the A operand
+//    (ds_read_b128, 16-B chunks XOR-swizzled by (key >> 1) & 7: conflict-free for the 32x32x16
+//    row pattern); V feeds O^T = V^T P^T through ds_read_b64_tr_b16, the hardware transpose read
+//    (chunks swizzled by ((key >> 1) & 1) << 2: conflict-free for its 4-row x 16-column blocks).
+//  * P never leaves registers: S^T's accumulator rows are the B operand of the P.V product.
 
-__global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 64 * FA_LDS];
-  bf16_t* Ks = smem;                 // [64 keys][72]   rows = key, cols = d
-  bf16_t* Vt = smem + 64 * FA_LDS;   // [64 d][72]      rows = d, cols = key
+#define FA_TILE 8192            // 64 keys x 128 B
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4_t lds_short4;
+
+__device__ __forceinline__ int fa_swk(int key) { return (key >> 1) & 7; }
+__device__ __forceinline__ int fa_swv(int key) { return ((key >> 1) & 1) << 2; }
+
+__global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p, unsigned k_bytes, unsigned v_bytes) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * FA_TILE];   // [buf][K | V]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int h = blockIdx.y, bat = blockIdx.z;
   const int q = blockIdx.x * 128 + wave * 32 + r32;
   const bf16_t* qb = (const bf16_t*)p.q + bat * p.bsq + h * 64;
-  const bf16_t* kb = (const bf16_t*)p.k + bat * p.bsk + h * 64;
-  const bf16_t* vb = (const bf16_t*)p.v + bat * p.bsv + h * 64;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((const bf16_t*)p.k + bat * p.bsk + h * 64), (short)0, (int)k_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((const bf16_t*)p.v + bat * p.bsv + h * 64), (short)0, (int)v_bytes, 0x00020000);
 
   // Q^T fragments as the B operand: lane holds Q[q][16s + 8hh + j]
   bf16x8_t qf[4];
@@ -41,35 +60,50 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
     qf[s] = *reinterpret_cast<bf16x8_t*>(&t);
   }
 
+  // DMA: wave w fills rows [8w, 8w+8) and [32 + 8w, +8) of each tile; lane -> (row, physical
+  // 16-B slot lane & 7) holding logical chunk slot ^ swizzle(row)
+  const int lrow = lane >> 3, slot = lane & 7;
+  int krow[2], kch[2], vch[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    krow[u] = (wave + 4 * u) * 8 + lrow;
+    kch[u] = slot ^ fa_swk(krow[u]);
+    vch[u] = slot ^ fa_swv(krow[u]);
+  }
+  auto stage = [&](int kv0, int buf) {
+    char* kt = smem + buf * 2 * FA_TILE;
+    char* vt = kt + FA_TILE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int key = kv0 + krow[u];
+      const unsigned ko = key < p.Skv ? ((unsigned)key * p.ldk + kch[u] * 8) * 2u : 0x80000000u;
+      const unsigned vo = key < p.Skv ? ((unsigned)key * p.ldv + vch[u] * 8) * 2u : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(kt + (wave + 4 * u) * 1024), 16, ko, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void*)(vt + (wave + 4 * u) * 1024), 16, vo, 0, 0, 0);
+    }
+  };
+
   const float c = p.scale * 1.4426950408889634f;   // fold log2(e): p = exp2(s*c - m)
   float m_run = -INFINITY, l_run = 0.0f;
   f32x16_t o0, o1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
 
+  // V transpose-read addressing: lane group g = lane / 16 covers d block (g & 1) * 16 (+32 for o1)
+  // and keys 8 * rd + 4 * (g >> 1) + qq of the 16-key step (the k order of S^T's accumulator rows,
+  // which are the B operand: element j of lane half h is key 8 * (j >> 2) + 4h + (j & 3)); lane
+  // 4qq + pp of the group supplies row qq, columns 4pp..4pp+3
+  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
+  const int tdcol = (tg & 1) * 16 + 4 * tp;          // d of this lane's 8-byte piece (o0)
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int buf = 0;
   for (int kv0 = 0; kv0 < p.Skv; kv0 += 64) {
-    // ---- stage K (row-major) and V^T into LDS ----
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cidx = tid + 256 * i;
-      // K: chunk-fastest mapping (coalesced rows)
-      {
-        const int row = cidx >> 3, kc = cidx & 7;
-        uint4 t = make_uint4(0, 0, 0, 0);
-        if (kv0 + row < p.Skv) t = *reinterpret_cast<const uint4*>(kb + (size_t)(kv0 + row) * p.ldk + kc * 8);
-        *reinterpret_cast<uint4*>(&Ks[row * FA_LDS + kc * 8]) = t;
-      }
-      // V: key-fastest mapping so the transposed 2-byte stores are bank-conflict free
-      {
-        const int row = cidx & 63, kc = cidx >> 6;
-        uint4 t = make_uint4(0, 0, 0, 0);
-        if (kv0 + row < p.Skv) t = *reinterpret_cast<const uint4*>(vb + (size_t)(kv0 + row) * p.ldv + kc * 8);
-        const bf16_t* e = reinterpret_cast<const bf16_t*>(&t);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) Vt[(kc * 8 + j) * FA_LDS + row] = e[j];
-      }
-    }
-    __syncthreads();
+    if (kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
+    const char* kt = smem + buf * 2 * FA_TILE;
+    const char* vt = kt + FA_TILE;
 
     // ---- S^T = K Q^T for two 32-key subtiles ----
     f32x16_t st[2];
@@ -77,28 +111,30 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
     for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[sub][r] = 0.0f;
-      const bf16_t* kr = Ks + (sub * 32 + r32) * FA_LDS + 8 * hh;
+      const int key = sub * 32 + r32;
+      const char* kr = kt + key * 128;
+      const int sk = fa_swk(key);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kr + 16 * s);
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4));
         st[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], st[sub], 0, 0, 0);
       }
     }
     // ---- online softmax (lane = query column) ----
     float mx = -INFINITY;
+    const bool ragged = kv0 + 64 > p.Skv;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int key = kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
         float sv = st[sub][r] * c;
-        if (key >= p.Skv) sv = -INFINITY;
+        if (ragged && kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) sv = -INFINITY;
         st[sub][r] = sv;
         mx = fmaxf(mx, sv);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     l_run *= alpha;
 #pragma unroll
@@ -112,29 +148,44 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float p0 = exp2f(st[sub][8 * s2 + 2 * j] - m_new);
-          const float p1 = exp2f(st[sub][8 * s2 + 2 * j + 1] - m_new);
+          const float p0 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j] - m_new);
+          const float p1 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j + 1] - m_new);
           l_run += p0 + p1;
           w[j] = pack2(p0, p1);
         }
         pf[sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
       }
-    // ---- O^T += V^T P^T ----
+    // ---- O^T += V^T P^T: A operand (d rows x 16 keys) by transpose reads of row-major V ----
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const int kbase = sub * 32 + 16 * s2 + 4 * hh;
-        uint2 lo0 = *reinterpret_cast<const uint2*>(&Vt[r32 * FA_LDS + kbase]);
-        uint2 hi0 = *reinterpret_cast<const uint2*>(&Vt[r32 * FA_LDS + kbase + 8]);
-        uint2 lo1 = *reinterpret_cast<const uint2*>(&Vt[(32 + r32) * FA_LDS + kbase]);
-        uint2 hi1 = *reinterpret_cast<const uint2*>(&Vt[(32 + r32) * FA_LDS + kbase + 8]);
-        uint4 a0 = make_uint4(lo0.x, lo0.y, hi0.x, hi0.y);
-        uint4 a1 = make_uint4(lo1.x, lo1.y, hi1.x, hi1.y);
-        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8_t*>(&a0), pf[sub][s2], o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8_t*>(&a1), pf[sub][s2], o1, 0, 0, 0);
+        short4_t t[2][2];
+#pragma unroll
+        for (int rd = 0; rd < 2; ++rd) {
+          const int key = sub * 32 + 16 * s2 + 8 * rd + 4 * (tg >> 1) + tq;
+          const int sv = fa_swv(key);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) {
+            const int d = tdcol + 32 * dh;
+            const char* a = vt + key * 128 + ((((d >> 3) ^ sv)) << 4) + (d & 7) * 2;
+            t[dh][rd] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)a);
+          }
+        }
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          short4_t lo = t[dh][0], hi = t[dh][1];
+          typedef short short8_t __attribute__((ext_vector_type(8)));
+          short8_t v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8_t af = *reinterpret_cast<bf16x8_t*>(&v8);
+          if (dh == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[sub][s2], o0, 0, 0, 0);
+          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[sub][s2], o1, 0, 0, 0);
+        }
       }
-    __syncthreads();
+    // next tile landed (this wave's DMAs) and every wave is done reading `buf`
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    buf ^= 1;
   }
 
   l_run += __shfl_xor(l_run, 32, 64);
@@ -159,8 +210,11 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
   if (d->Sq <= 0 || d->Skv <= 0 || d->nheads <= 0 || d->nbatch <= 0) return ACTH_EINVAL;
   if (d->ldq % 8 || d->ldk % 8 || d->ldv % 8 || d->ldo % 4) return ACTH_EINVAL;
   if (d->nheads > 65535 || d->nbatch > 65535) return ACTH_EINVAL;
+  // K / V buffer extents seen from one (batch, head) base: rows x ld, minus the head offset
+  const long long kb = ((long long)(d->Skv - 1) * d->ldk + 64) * 2, vb = ((long long)(d->Skv - 1) * d->ldv + 64) * 2;
+  if (kb >= 0x80000000LL || vb >= 0x80000000LL) return ACTH_EINVAL;
   dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
-  hipLaunchKernelGGL(flash_attn_kernel, grid, dim3(256), 0, stream, *d);
+  hipLaunchKernelGGL(flash_attn_kernel, grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

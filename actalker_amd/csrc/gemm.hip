@@ -9,7 +9,7 @@
 //       temporal3 : A[m, kf*Cin + c] = x[(b,f+kf-1,s), c]          (Conv3d kernel (3,1,1))
 //     each loader can read its K range from two tensors (channel concat of UNet skips).
 //   * epilogue: alpha*acc + bias[n] + rowbias[row/rb_div, n] + R[rmap(row), n],
-//     optional SiLU / GELU / GEGLU (h * gelu(g) on interleaved 32-column granules),
+//     optional SiLU / GELU / GEGLU (h * gelu(g) on interleaved 16-column granules),
 //     optional AlphaBlender mix with a second tensor, fp32 or bf16 output, row remap.
 //
 // Structure: 128x128x64 workgroup tile, 4 waves (2x2), each wave 64x64 = 2x2 tiles of
@@ -155,11 +155,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
     const int row = tile_m + r0;
     if (row >= p.M) break;
     if (geglu) {
-      // output columns [tile_n/2 + 8cg, +8): hidden at tile col 64g + j, gate at 64g + 32 + j
+      // output columns [tile_n/2 + 8cg, +8): hidden at tile col 32g + j, gate at 32g + 16 + j
       const int oc = cg * 8;
-      const int hc = 64 * (oc >> 5) + (oc & 31);
-      if (tile_n + hc + 32 >= p.N) continue;
-      epilogue_geglu8(p, row, tile_n + hc, tile_n / 2 + oc, &et[r0 * EPI_LD + hc], &et[r0 * EPI_LD + hc + 32], vec_ok);
+      const int hc = 32 * (oc >> 4) + (oc & 15);
+      if (tile_n + hc + 16 >= p.N) continue;
+      epilogue_geglu8(p, row, tile_n + hc, tile_n + hc + 16, tile_n / 2 + oc, &et[r0 * EPI_LD + hc],
+                      &et[r0 * EPI_LD + hc + 16], vec_ok);
     } else {
       const int c0 = cg * 8;
       const int ocol = tile_n + c0;
@@ -175,21 +176,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
 
 int gemm256_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                    int vec_ok, hipStream_t stream);
+int gemm8p_launch(const ActhGemmDesc* d, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes, int vec_ok,
+                  hipStream_t stream);
 
-// Tile choice by a rounds x tile-area cost: 256-row tiles run one workgroup per CU (256 slots),
-// the 128x128 kernel two (512 slots) at ~2/3 of the big tiles' MFMA efficiency; between the
-// 256- and 160-column variants the one wasting fewer padded columns wins (160 divides 320/640/960).
+// Tile choice (measured on MI355X, tools/bench_gemm.py): the phased 256x256 kernel wherever it
+// fills the chip; the persistent 256x160 kernel for N <= 320 (160 divides the C = 320 projections,
+// where a 256-column tile would waste 37.5 %) and for grids too small for 256x256 tiles; the 128x128
+// kernel for small M or N.
 static int choose_tile(const ActhGemmDesc* d) {
   if (d->tile) return d->tile & 0xff;
   if (d->N < 128 || d->M < 256) return 1;
   const long long mt = (d->M + 255) / 256;
-  const long long b2 = mt * ((d->N + 255) / 256), b3 = mt * ((d->N + 159) / 160);
-  const long long b1 = ((d->M + 127) / 128) * ((d->N + 127) / 128);
-  const double c2 = (double)((b2 + 255) / 256) * 65536.0;
-  const double c3 = d->act == 2 ? 1e30 : (double)((b3 + 255) / 256) * 40960.0;
-  const double c1 = (double)((b1 + 511) / 512) * 16384.0 * 1.5;
-  if (c1 < c2 && c1 < c3) return 1;
-  return c3 < c2 ? 3 : 2;
+  if (d->act == 2) return (d->N % 256 == 0 && mt * (d->N / 256) >= 256) ? 4 : 1;
+  if (d->N <= 320 || mt * ((d->N + 255) / 256) < 256) return 3;
+  return 4;
 }
 
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
@@ -205,7 +205,7 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   if (d->amode != 0 && (d->Cin % BKT || d->K % d->Cin)) return ACTH_EINVAL;
   if (d->amode == 1 && d->K != 9 * d->Cin) return ACTH_EINVAL;
   if (d->amode == 2 && (d->K != 3 * d->Cin || d->F <= 0 || d->S <= 0)) return ACTH_EINVAL;
-  if (d->act == 2 && d->N % 64) return ACTH_EINVAL;
+  if (d->act == 2 && d->N % 32) return ACTH_EINVAL;
   if (d->orow_div <= 0 || (d->rowbias && d->rb_div <= 0) || (d->rmap && (d->r_div <= 0 || d->r_mod <= 0)))
     return ACTH_EINVAL;
   // operand extents (buffer num_records): rows of each A source and of B
@@ -219,6 +219,7 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   const long long b_bytes = ((long long)(d->N - 1) * d->ldb + d->K) * 2;
   if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) return ACTH_EINVAL;
   const int tile = choose_tile(d) & 0xff;
+  if (tile == 4) return gemm8p_launch(d, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
   if (tile == 2 || tile == 3)
     return gemm256_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
   if (tile != 1) return ACTH_EINVAL;

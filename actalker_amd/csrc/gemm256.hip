@@ -236,13 +236,14 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(const ActhGemmDesc p, u
       // the slab is private to this wave and LDS ops of one wave complete in order
       const int rbase = row0 + i * 16;
       if (geglu) {
-        // one 64-column granule per wave: hidden cols [0, 32), gate cols [32, 64) -> 32 outputs
+        // two (hidden 16 | gate 16) granule pairs per wave -> 32 outputs: 16 rows x 4 chunks
         if (WTN == 64 && col0 < p.N) {
           const int r = lane >> 2, oc = (lane & 3) * 8;
+          const int hc = 32 * (oc >> 4) + (oc & 15);
           const int row = rbase + r;
           if (row < p.M)
-            epilogue_geglu8(p, row, col0 + oc, col0 / 2 + oc, &et[r * EPI_LD + oc], &et[r * EPI_LD + 32 + oc],
-                            vec_ok);
+            epilogue_geglu8(p, row, col0 + hc, col0 + hc + 16, col0 / 2 + oc, &et[r * EPI_LD + hc],
+                            &et[r * EPI_LD + hc + 16], vec_ok);
         }
       } else {
         constexpr int CPR = WTN / 8;             // 8-column chunks per row

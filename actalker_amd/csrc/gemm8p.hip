@@ -1,0 +1,303 @@
+// bf16 MFMA GEMM, 256x256 tile, 8 waves, 4-phase-per-K-tile interleaved schedule (gfx950).
+//
+// Same operands, loaders and fused epilogues as gemm.hip / gemm256.hip (gemm_common.h); this is
+// the main-loop schedule of the CDNA4 "8-phase" GEMM template (cdna_hip_programming.md §5,
+// T2+T3+T4+T5): each 64-deep K tile is split into 4 phases, one per quadrant of the 256x256 block
+// tile; in a phase every wave computes its 64x32 share of that quadrant (4x2 fragments x 2 k-steps
+// = 16 v_mfma_f32_16x16x32_bf16), so a phase needs only one A half-tile (128 rows) and one B
+// half-tile (128 columns). Quadrant order (0,0) (0,1) (1,1) (1,0) means fragments are re-read only
+// when their half changes (12, 4, 8, 4 ds_read_b128 per phase).
+//
+// Staging: the next K tile's four 16 KB half-tiles are LDS-DMA'd one per phase (2 wave-instructions
+// per wave), in the order they are first needed (A0 B0 B1 A1), into the other of two 64 KB buffers,
+// and waited for with a counted `s_waitcnt vmcnt(2)` one phase before their first reader, so loads
+// stay in flight across barriers (never vmcnt(0) in the loop).
+//
+// Wave stagger: waves 4-7 run one barrier behind waves 0-3, so on every SIMD (which hosts one wave
+// of each half) one wave's ds_read + DMA issue segment overlaps the other's MFMA segment. Hazards
+// under the stagger (one barrier = half a phase): a half-tile is read >= one phase after the last
+// wait that retires it; a buffer is re-staged >= two phases after its last read.
+#include "gemm_common.h"
+
+using namespace gemm;
+
+namespace {
+
+template <int AMODE>
+__device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, int m, const RowInfo& ri, int tap) {
+  if (!ri.ok) return -1;
+  if (AMODE == 0) return m;
+  if (AMODE == 1) {
+    const int ky = tap / 3, kx = tap - ky * 3;
+    int iy, ix;
+    if (p.upsample) {
+      iy = ri.y + ky - 1; ix = ri.x + kx - 1;
+      if (iy < 0 || ix < 0 || iy >= 2 * p.H || ix >= 2 * p.W) return -1;
+      iy >>= 1; ix >>= 1;
+    } else {
+      iy = ri.y * p.conv_stride + ky - 1; ix = ri.x * p.conv_stride + kx - 1;
+      if (iy < 0 || ix < 0 || iy >= p.H || ix >= p.W) return -1;
+    }
+    return (ri.b * p.H + iy) * p.W + ix;
+  }
+  const int f = ri.y + tap - 1;
+  if (f < 0 || f >= p.F) return -1;
+  return m + (tap - 1) * p.S;
+}
+
+#define BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
+                   __builtin_amdgcn_sched_barrier(0); } while (0)
+
+}  // namespace
+
+template <int AMODE>
+__global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, unsigned a_bytes, unsigned a2_bytes,
+                                                        unsigned b_bytes, int vec_ok) {
+  constexpr int HALF = 16384;                   // one 128-row x 64-k half-tile
+  constexpr int BUF = 4 * HALF;                 // A0 A1 B0 B1
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave & 1, wc = wave >> 1;      // wave's row / column slot inside a quadrant
+  const bool late = wave >= 4;                  // staggered half
+
+  // XCD-aware bijective tile order (n fastest), as gemm.hip
+  const int ntn = gridDim.x;
+  const int nwg = gridDim.x * gridDim.y;
+  const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int tile_n = (lin % ntn) * 256;
+  const int tile_m = (lin / ntn) * 256;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(p.A2 ? p.A2 : p.A, p.A2 ? a2_bytes : 0u);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
+
+  // DMA: half-tile piece i (0..15) = rows [8i, 8i+8); wave w issues pieces w and w + 8.
+  // Lane -> (row 8i + lane/8, physical 16-B slot lane%8) holding logical K chunk slot ^ (row & 7).
+  const int lrow = lane >> 3;
+  const int cch = (lane & 7) ^ lrow;
+  // rows [h][u]: half h, piece w + 8u
+  RowInfo ri[2][2];
+  int arow[2][2];
+  unsigned aoff[2][2], aoff2[2][2], boff[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      arow[h][u] = tile_m + h * 128 + (wave + 8 * u) * 8 + lrow;
+      ri[h][u] = row_info(p, arow[h][u]);
+      const int brow = tile_n + h * 128 + (wave + 8 * u) * 8 + lrow;
+      boff[h][u] = brow < p.N ? ((unsigned)brow * p.ldb + cch * 8) * 2u : OOB;
+    }
+  auto set_tap = [&](int tap) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int pix = tap_pixel8<AMODE>(p, arow[h][u], ri[h][u], tap);
+        aoff[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda + cch * 8) * 2u;
+        aoff2[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda2 + cch * 8) * 2u;
+      }
+  };
+  set_tap(0);
+  const bool two_src = p.A2 != nullptr;
+  const int cin = AMODE == 0 ? 0x7fffffff : p.Cin;
+  const int nk = (p.K + 63) / 64;
+  const int kfull = p.K / 64;
+
+  // per-K-tile staging parameters, advanced by prep_k() in K order
+  int s_tap = 0, s_c0 = 0;
+  int k_c0 = 0, k_k0 = 0;
+  bool k_second = false, k_tail = false;
+  auto prep_k = [&](int kt) {
+    k_k0 = kt * 64;
+    if (AMODE == 0) {
+      k_c0 = k_k0;
+    } else {
+      if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
+      k_c0 = s_c0;
+      s_c0 += 64;
+      if (s_c0 == cin) { s_c0 = 0; ++s_tap; }
+    }
+    k_second = two_src && k_c0 >= p.K1;
+    k_tail = kt >= kfull;
+  };
+  auto stage_a = [&](int h, int buf) {
+    char* dst0 = smem + buf * BUF + h * HALF;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      unsigned off = k_second ? aoff2[h][u] + (unsigned)(k_c0 - p.K1) * 2u : aoff[h][u] + (unsigned)k_c0 * 2u;
+      if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
+      lds_void* dst = (lds_void*)(dst0 + (wave + 8 * u) * 1024);
+      if (k_second) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra2, dst, 16, off, 0, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, off, 0, 0, 0);
+    }
+  };
+  auto stage_b = [&](int h, int buf) {
+    char* dst0 = smem + buf * BUF + (2 + h) * HALF;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      unsigned off = boff[h][u] + (unsigned)k_k0 * 2u;
+      if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + (wave + 8 * u) * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
+  // fragment reads: row base + 16 t + lane%16, swizzle key row & 7 == lane & 7
+  const int fr = lane & 15, fkey = lane & 7, fq = lane >> 4;
+  const int sw0 = ((0 + fq) ^ fkey) << 4, sw1 = ((4 + fq) ^ fkey) << 4;
+  const int a_row = (wr * 64 + fr) * 128;       // inside an A half
+  const int b_row = (wc * 32 + fr) * 128;       // inside a B half
+
+  f32x4_t acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+  bf16x8_t af[4][2], bfr[2][2];
+
+  auto read_a = [&](int buf, int h) {
+    const char* s = smem + buf * BUF + h * HALF + a_row;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw0);
+      af[i][1] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw1);
+    }
+  };
+  auto read_b = [&](int buf, int h) {
+    const char* s = smem + buf * BUF + (2 + h) * HALF + b_row;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bfr[j][0] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw0);
+      bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw1);
+    }
+  };
+  auto mma = [&](f32x4_t (&c)[4][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K tile 0 fully staged and landed
+  prep_k(0);
+  stage_a(0, 0); stage_b(0, 0); stage_b(1, 0); stage_a(1, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  BAR();
+  if (late) BAR();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1, nxt = cur ^ 1;
+    const bool more = kt + 1 < nk;
+    if (more) prep_k(kt + 1);
+    // phase 0: quadrant (0,0); stage A0(k+1)
+    read_a(cur, 0); read_b(cur, 0);
+    if (more) stage_a(0, nxt);
+    BAR();
+    mma(acc[0][0]);
+    // A1(k) is read in phase 2: retire it now (DMA'd in the previous tile's phase 3)
+    if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    BAR();
+    // phase 1: quadrant (0,1); stage B0(k+1)
+    read_b(cur, 1);
+    if (more) stage_b(0, nxt);
+    BAR();
+    mma(acc[0][1]);
+    BAR();
+    // phase 2: quadrant (1,1); stage B1(k+1)
+    read_a(cur, 1);
+    if (more) stage_b(1, nxt);
+    BAR();
+    mma(acc[1][1]);
+    // A0(k+1), B0(k+1) are read in the next tile's phase 0
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    BAR();
+    // phase 3: quadrant (1,0); stage A1(k+1)
+    read_b(cur, 0);
+    if (more) stage_a(1, nxt);
+    BAR();
+    mma(acc[1][0]);
+    // B1(k+1) is read in the next tile's phase 1
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    BAR();
+  }
+  if (!late) BAR();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  BAR();
+
+  // ---- epilogue: per quadrant, the wave's 64 x 32 accumulators -> private LDS slab -> 8-column
+  // row chunks (16-byte coalesced epilogue loads / stores). (Storing straight from the fragments,
+  // 8 bytes per lane across 16 rows, measured up to 1.7x slower on the small-K shapes.)
+  constexpr int EPI_LD = 36;                    // fp32 stride of a wave's 64 x 32 slab
+  float* et = reinterpret_cast<float*>(smem) + wave * (64 * EPI_LD);
+  const bool geglu = p.act == 2;
+  auto flush = [&](int qm, int qn) {
+    const int row0 = tile_m + qm * 128 + wr * 64;
+    const int col0 = tile_n + qn * 128 + wc * 32;
+    if (geglu) {
+      // one (hidden 16 | gate 16) granule pair -> 16 outputs: 64 rows x 2 chunks
+#pragma unroll 1
+      for (int ch = lane; ch < 128; ch += 64) {
+        const int r = ch >> 1, oc = (ch & 1) * 8;
+        if (row0 + r < p.M && col0 < p.N)
+          epilogue_geglu8(p, row0 + r, col0 + oc, col0 + 16 + oc, col0 / 2 + oc, &et[r * EPI_LD + oc],
+                          &et[r * EPI_LD + 16 + oc], vec_ok);
+      }
+    } else {
+#pragma unroll 1
+      for (int ch = lane; ch < 256; ch += 64) {
+        const int r = ch >> 2, c8 = (ch & 3) * 8;
+        const int ocol = col0 + c8;
+        if (row0 + r < p.M && ocol < p.N) {
+          float v[8];
+          const float4 x0 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8]);
+          const float4 x1 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8 + 4]);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+          epilogue8(p, row0 + r, ocol, v, vec_ok);
+        }
+      }
+    }
+  };
+  auto slab = [&](const f32x4_t (&c)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) et[(i * 16 + fq * 4 + r) * EPI_LD + j * 16 + fr] = c[i][j][r];
+  };
+  // the slab is private to this wave and LDS ops of one wave complete in order
+  slab(acc[0][0]); flush(0, 0);
+  slab(acc[0][1]); flush(0, 1);
+  slab(acc[1][0]); flush(1, 0);
+  slab(acc[1][1]); flush(1, 1);
+}
+
+int gemm8p_launch(const ActhGemmDesc* d, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes, int vec_ok,
+                  hipStream_t stream) {
+  const int mt = (d->M + 255) / 256;
+  if (mt > 65535) return ACTH_EINVAL;
+  const dim3 grid((d->N + 255) / 256, mt);
+  if (d->amode == 1)
+    hipLaunchKernelGGL(gemm8p_kernel<1>, grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+  else if (d->amode == 2)
+    hipLaunchKernelGGL(gemm8p_kernel<2>, grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+  else
+    hipLaunchKernelGGL(gemm8p_kernel<0>, grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}

@@ -71,6 +71,18 @@ __device__ __forceinline__ bool second_source(const ActhGemmDesc& p, int k0) {
   return p.A2 && ((p.amode == 0 ? k0 : k0 % p.Cin) >= p.K1);
 }
 
+// v[e] += src[e] for e < 8 (or e < n when !vec): two float4 loads when 16-byte aligned
+__device__ __forceinline__ void add8(float* v, const float* src, bool vec, int n) {
+  if (vec) {
+    const float4 a = reinterpret_cast<const float4*>(src)[0];
+    const float4 b = reinterpret_cast<const float4*>(src)[1];
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += e < n ? src[e] : 0.0f;
+  }
+}
+
 __device__ __forceinline__ size_t out_row(const ActhGemmDesc& p, int row) {
   return (size_t)(row / p.orow_div) * p.orow_stride + (row % p.orow_div) + p.orow_off;
 }
@@ -101,14 +113,10 @@ __device__ __forceinline__ void epilogue8(const ActhGemmDesc& p, int row, int oc
   const bool vec = full && vec_ok;
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
-  if (p.bias) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += (ocol + e < p.N) ? p.bias[ocol + e] : 0.0f;
-  }
+  if (p.bias) add8(v, p.bias + ocol, full && !((size_t)(p.bias + ocol) & 15), p.N - ocol);
   if (p.rowbias) {
     const float* rb2 = p.rowbias + (size_t)(row / p.rb_div) * p.ldrb + ocol;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += (ocol + e < p.N) ? rb2[e] : 0.0f;
+    add8(v, rb2, full && !((size_t)rb2 & 15), p.N - ocol);
   }
   if (p.R) {
     size_t rrow = row;
@@ -146,18 +154,21 @@ __device__ __forceinline__ void epilogue8(const ActhGemmDesc& p, int row, int oc
   store8(p, out_row(p, row), ocol, v, full, vec_ok);
 }
 
-// GEGLU epilogue: hidden h[8] at weight columns [hcol, hcol+8) and gate g[8] at hcol + 32
-// (interleaved 32-column granules); writes h * gelu(g) at output column `ocol`.
-__device__ __forceinline__ void epilogue_geglu8(const ActhGemmDesc& p, int row, int hcol, int ocol, const float* h,
-                                                const float* g, int vec_ok) {
-  float v[8];
+// GEGLU epilogue: hidden h[8] at weight columns [hcol, hcol+8) and gate g[8] at [gcol, gcol+8)
+// (16-column granules, modules.pack_geglu); writes h * gelu(g) at output column `ocol`.
+__device__ __forceinline__ void epilogue_geglu8(const ActhGemmDesc& p, int row, int hcol, int gcol, int ocol,
+                                                const float* h, const float* g, int vec_ok) {
+  float v[8], hv[8], gv[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float hv = h[e] * p.alpha + (p.bias ? p.bias[hcol + e] : 0.0f);
-    const float gv = g[e] * p.alpha + (p.bias ? p.bias[hcol + 32 + e] : 0.0f);
-    v[e] = hv * gelu_erf(gv);
+  for (int e = 0; e < 8; ++e) { hv[e] = h[e] * p.alpha; gv[e] = g[e] * p.alpha; }
+  if (p.bias) {
+    add8(hv, p.bias + hcol, !((size_t)(p.bias + hcol) & 15), 8);
+    add8(gv, p.bias + gcol, !((size_t)(p.bias + gcol) & 15), 8);
   }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = hv[e] * gelu_erf(gv[e]);
   store8(p, out_row(p, row), ocol, v, true, vec_ok);
 }
+
 
 }  // namespace gemm

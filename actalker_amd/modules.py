@@ -68,13 +68,19 @@ def pack_conv3d_t(w: torch.Tensor) -> torch.Tensor:
     return _bf(w[:, :, :, 0, 0].permute(0, 2, 1).reshape(w.shape[0], -1))
 
 
+GEGLU_G = 16   # GEGLU granule: the GEMM epilogues pair hidden column j with gate column j + 16
+
+
 def pack_geglu(w: torch.Tensor, b: torch.Tensor):
-    """GEGLU proj (2*I, C) [hidden; gate] -> rows interleaved in 32-row granules [h32, g32, h32, ...]."""
+    """GEGLU proj (2*I, C) [hidden; gate] -> rows interleaved in 16-row granules [h16, g16, h16, ...], so
+    every 32 consecutive GEMM output columns hold 16 hidden and their 16 gate columns (the 16x16 MFMA
+    fragment width): the GELU gate fuses into the GEMM epilogue."""
     inner = w.shape[0] // 2
+    G = GEGLU_G
     hw, gw = w[:inner], w[inner:]
     hb, gb = b[:inner], b[inner:]
-    wi = torch.stack([hw.view(inner // 32, 32, -1), gw.view(inner // 32, 32, -1)], 1).reshape(2 * inner, -1)
-    bi = torch.stack([hb.view(inner // 32, 32), gb.view(inner // 32, 32)], 1).reshape(-1)
+    wi = torch.stack([hw.view(inner // G, G, -1), gw.view(inner // G, G, -1)], 1).reshape(2 * inner, -1)
+    bi = torch.stack([hb.view(inner // G, G), gb.view(inner // G, G)], 1).reshape(-1)
     return _bf(wi), _f32(bi)
 
 

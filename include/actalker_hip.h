@@ -47,11 +47,11 @@ typedef struct ActhGemmDesc {
   const void* R; int ldr; const int* rmap; int r_div, r_mod;
   const void* MIX; int ldmix; float mix_alpha;
   float alpha;
-  int act;                   /* 0 none, 1 silu, 2 geglu (interleaved 32-col granules), 3 gelu */
+  int act;                   /* 0 none, 1 silu, 2 geglu (interleaved 16-col granules), 3 gelu */
   int out_f32;
   void* C; int ldc;
   int orow_div, orow_stride, orow_off;
-  int tile;                  /* 0 auto; 1 128x128 (4 waves); 2 256x256, 3 256x160 (8 waves) */
+  int tile;                  /* 0 auto; 1 128x128 (4 waves); 2 256x256, 3 256x160, 4 256x256 phased (8 waves) */
 } ActhGemmDesc;
 int acth_gemm(const ActhGemmDesc* d, hipStream_t stream);
 int acth_gemm_desc_size(void);

@@ -94,7 +94,7 @@ def test_gemm_geglu_and_orow(dev):
     assert float(got[0:3].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
 def test_gemm_tile_variants(dev, tile):
     """Every tile kernel (128x128; 256x256 and 256x160 8-wave) on all A loaders, tails and epilogues."""
     from actalker_amd.modules import pack_conv3x3, pack_conv3d_t, pack_geglu
@@ -138,7 +138,7 @@ def test_gemm_tile_variants(dev, tile):
     out = ops.gemm(tk.to(dev), pack_conv3d_t(wt).to(dev), temporal=dict(F=Ft, S=S), tile=tile)
     refo = F.conv3d(x.float(), wt.float(), None, padding=(1, 0, 0)).permute(0, 2, 3, 4, 1).reshape(-1, Co)
     assert rel(out, refo) < 1e-2
-    # GEGLU (the 256x160 tile rejects it: its wave tiles are not 64-column granules)
+    # GEGLU (the 256x160 tile rejects it: its wave tiles do not hold whole hidden|gate granule pairs)
     Mg, Cg, inner = 600, 192, 640
     xg = bf(rnd(Mg, Cg))
     wg, bg = rnd(2 * inner, Cg, scale=Cg ** -0.5), rnd(2 * inner, scale=0.1)

@@ -189,8 +189,9 @@ extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
 // Input may be the channel concat of x (C1 channels) and x2 (C - C1 channels).
 
 // Statistics: each block reduces GS_ROWS rows of one statistics batch to per-channel fp32 partial
-// sums (LDS), folds them to per-group sums and adds those to fp64 accumulators (2*G doubles per
-// batch). Apply: each block covers rows of a single batch, turns (mean, rstd, gamma, beta) into a
+// sums (LDS), folds them in a fixed order to per-group fp64 sums and adds those to fp64
+// accumulators (2*G doubles per batch; fp64 sums of fp32 partials are exact in practice, so the
+// cross-block atomics do not make the result order-dependent). Apply: each block covers rows of a single batch, turns (mean, rstd, gamma, beta) into a
 // per-channel scale/shift once, then streams y = x * a + b (+ SiLU) with 16-byte accesses.
 // Thread layout of both: nchl = min(C/8, 256) chunk columns x (256 / nchl) row lanes; a thread
 // owns chunk columns cl and cl + nchl (C <= 4096).
@@ -205,13 +206,13 @@ __device__ __forceinline__ uint4 gn_load(const ActhGroupNormDesc& p, long long r
 
 // grid: (ceil(rows_per_stat / GS_ROWS), nstat)
 __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p) {
-  __shared__ float red[2 * 4096];
+  // per row lane, per channel partial sums (written once each, reduced in a fixed order below, so
+  // the statistics are bit-reproducible): rows_par * 2C <= 8192 floats for C <= 4096
+  __shared__ float red[8192];
   const int nch = p.C >> 3;
   const int nchl = nch < 256 ? nch : 256;
   const int rows_par = 256 / nchl;
   const int t = threadIdx.x;
-  for (int c = t; c < 2 * p.C; c += 256) red[c] = 0.0f;
-  __syncthreads();
   const int stat = blockIdx.y;
   const long long r_begin = (long long)stat * p.rows_per_stat + (long long)blockIdx.x * GS_ROWS;
   const long long r_end = min((long long)stat * p.rows_per_stat + p.rows_per_stat, r_begin + GS_ROWS);
@@ -240,18 +241,17 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p
 #pragma unroll
         for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
       }
+      float* dst = red + rl * 2 * p.C + ch * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        atomicAdd(&red[ch * 8 + e], s1[e]);
-        atomicAdd(&red[p.C + ch * 8 + e], s2[e]);
-      }
+      for (int e = 0; e < 8; ++e) { dst[e] = s1[e]; dst[p.C + e] = s2[e]; }
     }
   }
   __syncthreads();
   const int cpg = p.C / p.G;
   if (t < p.G) {
     double a1 = 0.0, a2 = 0.0;
-    for (int c = t * cpg; c < (t + 1) * cpg; ++c) { a1 += red[c]; a2 += red[p.C + c]; }
+    for (int r = 0; r < rows_par; ++r)
+      for (int c = t * cpg; c < (t + 1) * cpg; ++c) { a1 += red[r * 2 * p.C + c]; a2 += red[r * 2 * p.C + p.C + c]; }
     double* acc = p.ws + ((size_t)stat * p.G + t) * 2;
     atomicAdd(acc, a1);
     atomicAdd(acc + 1, a2);

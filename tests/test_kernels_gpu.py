@@ -281,6 +281,24 @@ def test_groupnorm(dev, C1, C2, silu, temporal):
     if silu:
         yr = F.silu(yr)
     assert rel(out, yr.permute(0, 2, 1).reshape(-1, C)) < 1e-2
+    # bit-reproducible (fixed-order block reductions; fp64 cross-block sums)
+    for _ in range(3):
+        again = ops.groupnorm(x1.to(dev), g.to(dev), b.to(dev), 1e-6, rps, x2=None if x2 is None else x2.to(dev),
+                              silu=silu)
+        assert torch.equal(again, out)
+
+
+def test_groupnorm_large_rows_reproducible(dev):
+    """Level-0 sized statistics batches (many stats blocks per batch, 320 channels)."""
+    M, C, rps = 2 * 9216, 320, 9216
+    x = bf(rnd(M, C, scale=3.0) + 1.0).to(dev)
+    g, b = rnd(C).to(dev), rnd(C).to(dev)
+    out = ops.groupnorm(x, g, b, 1e-6, rps, silu=True)
+    xr = x.float().cpu().view(2, rps, C).permute(0, 2, 1)
+    ref_y = F.silu(F.group_norm(xr, 32, g.cpu(), b.cpu(), 1e-6)).permute(0, 2, 1).reshape(M, C)
+    assert rel(out, ref_y) < 1e-2
+    for _ in range(3):
+        assert torch.equal(ops.groupnorm(x, g, b, 1e-6, rps, silu=True), out)
 
 
 # ------------------------------------------------------------------------------------------ scan

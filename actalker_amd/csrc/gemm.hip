@@ -176,20 +176,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
 
 int gemm256_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                    int vec_ok, hipStream_t stream);
-int gemm8p_launch(const ActhGemmDesc* d, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes, int vec_ok,
-                  hipStream_t stream);
+int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
+                  int vec_ok, hipStream_t stream);
 
-// Tile choice (measured on MI355X, tools/bench_gemm.py): the phased 256x256 kernel wherever it
-// fills the chip; the persistent 256x160 kernel for N <= 320 (160 divides the C = 320 projections,
-// where a 256-column tile would waste 37.5 %) and for grids too small for 256x256 tiles; the 128x128
-// kernel for small M or N.
+// Tile choice (measured on MI355X, tools/bench_gemm.py): the phased 256x320 kernel for every
+// non-GEGLU GEMM that fills the chip (every UNet width is a multiple of 320), the phased 256x256
+// kernel for GEGLU (its wave tiles hold whole hidden|gate granule pairs), the persistent 256x160
+// kernel for grids too small for either, the 128x128 kernel for small M or N.
 static int choose_tile(const ActhGemmDesc* d) {
   if (d->tile) return d->tile & 0xff;
   if (d->N < 128 || d->M < 256) return 1;
   const long long mt = (d->M + 255) / 256;
   if (d->act == 2) return (d->N % 256 == 0 && mt * (d->N / 256) >= 256) ? 4 : 1;
-  if (d->N <= 320 || mt * ((d->N + 255) / 256) < 256) return 3;
-  return 4;
+  if (mt * ((d->N + 319) / 320) >= 256) return 5;
+  return 3;
 }
 
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
@@ -219,7 +219,8 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   const long long b_bytes = ((long long)(d->N - 1) * d->ldb + d->K) * 2;
   if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) return ACTH_EINVAL;
   const int tile = choose_tile(d) & 0xff;
-  if (tile == 4) return gemm8p_launch(d, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
+  if (tile == 4 || tile == 5)
+    return gemm8p_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
   if (tile == 2 || tile == 3)
     return gemm256_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
   if (tile != 1) return ACTH_EINVAL;

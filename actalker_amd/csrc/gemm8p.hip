@@ -50,18 +50,30 @@ __device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, int m, const Ro
 
 }  // namespace
 
-template <int AMODE>
+// BN_ = 256: waves 2 (rows) x 4 (cols), a wave's quadrant share is 64 x 32 (4 x 2 fragments);
+// BN_ = 320 (the C = 320 projections and convs, one tile spans N): waves 4 x 2, share 32 x 80
+// (2 x 5 fragments), B half-tiles of 160 rows (20 DMA pieces: waves 0-3 issue 3, waves 4-7 two).
+template <int BN_, int AMODE>
 __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, unsigned a_bytes, unsigned a2_bytes,
                                                         unsigned b_bytes, int vec_ok) {
-  constexpr int HALF = 16384;                   // one 128-row x 64-k half-tile
-  constexpr int BUF = 4 * HALF;                 // A0 A1 B0 B1
+  constexpr int WR = BN_ == 256 ? 2 : 4, WC = 8 / WR;
+  constexpr int TMQ = 128 / WR / 16, TNQ = BN_ / 2 / WC / 16;   // fragments per wave and quadrant
+  constexpr int AH = 128 * 128;                 // A half-tile: 128 rows x 64 k
+  constexpr int BH = BN_ / 2 * 128;             // B half-tile: BN/2 rows x 64 k
+  constexpr int BUF = 2 * AH + 2 * BH;          // A0 A1 B0 B1
+  constexpr int NBP = BN_ / 16;                 // DMA pieces per B half-tile
+  constexpr int NBJ = (NBP + 7) / 8;
+  static_assert(TMQ * WR * 16 == 128 && TNQ * WC * 16 == BN_ / 2, "quadrant split");
+  static_assert(2 * BUF <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave & 1, wc = wave >> 1;      // wave's row / column slot inside a quadrant
+  const int wr = wave % WR, wc = wave / WR;     // wave's row / column slot inside a quadrant
   const bool late = wave >= 4;                  // staggered half
+  // B-half DMA pieces this wave issues (wave + 8u < NBP): the count differs by wave when NBP % 8
+  const int nbw = (NBP - wave + 7) / 8;
 
   // XCD-aware bijective tile order (n fastest), as gemm.hip
   const int ntn = gridDim.x;
@@ -69,7 +81,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int bid = blockIdx.x + gridDim.x * blockIdx.y;
   const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
   const int lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int tile_n = (lin % ntn) * 256;
+  const int tile_n = (lin % ntn) * BN_;
   const int tile_m = (lin / ntn) * 256;
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
@@ -83,16 +95,20 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   // rows [h][u]: half h, piece w + 8u
   RowInfo ri[2][2];
   int arow[2][2];
-  unsigned aoff[2][2], aoff2[2][2], boff[2][2];
+  unsigned aoff[2][2], aoff2[2][2], boff[2][NBJ];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       arow[h][u] = tile_m + h * 128 + (wave + 8 * u) * 8 + lrow;
       ri[h][u] = row_info(p, arow[h][u]);
-      const int brow = tile_n + h * 128 + (wave + 8 * u) * 8 + lrow;
+    }
+#pragma unroll
+    for (int u = 0; u < NBJ; ++u) {
+      const int brow = tile_n + h * (BN_ / 2) + (wave + 8 * u) * 8 + lrow;
       boff[h][u] = brow < p.N ? ((unsigned)brow * p.ldb + cch * 8) * 2u : OOB;
     }
+  }
   auto set_tap = [&](int tap) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -127,7 +143,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     k_tail = kt >= kfull;
   };
   auto stage_a = [&](int h, int buf) {
-    char* dst0 = smem + buf * BUF + h * HALF;
+    char* dst0 = smem + buf * BUF + h * AH;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       unsigned off = k_second ? aoff2[h][u] + (unsigned)(k_c0 - p.K1) * 2u : aoff[h][u] + (unsigned)k_c0 * 2u;
@@ -138,56 +154,58 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     }
   };
   auto stage_b = [&](int h, int buf) {
-    char* dst0 = smem + buf * BUF + (2 + h) * HALF;
+    char* dst0 = smem + buf * BUF + 2 * AH + h * BH;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      unsigned off = boff[h][u] + (unsigned)k_k0 * 2u;
-      if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + (wave + 8 * u) * 1024), 16, off, 0, 0, 0);
+    for (int u = 0; u < NBJ; ++u) {
+      if (NBP % 8 == 0 || wave + 8 * u < NBP) {
+        unsigned off = boff[h][u] + (unsigned)k_k0 * 2u;
+        if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + (wave + 8 * u) * 1024), 16, off, 0, 0, 0);
+      }
     }
   };
 
   // fragment reads: row base + 16 t + lane%16, swizzle key row & 7 == lane & 7
   const int fr = lane & 15, fkey = lane & 7, fq = lane >> 4;
   const int sw0 = ((0 + fq) ^ fkey) << 4, sw1 = ((4 + fq) ^ fkey) << 4;
-  const int a_row = (wr * 64 + fr) * 128;       // inside an A half
-  const int b_row = (wc * 32 + fr) * 128;       // inside a B half
+  const int a_row = (wr * TMQ * 16 + fr) * 128;   // inside an A half
+  const int b_row = (wc * TNQ * 16 + fr) * 128;   // inside a B half
 
-  f32x4_t acc[2][2][4][2];
+  f32x4_t acc[2][2][TMQ][TNQ];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TMQ; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-  bf16x8_t af[4][2], bfr[2][2];
+        for (int j = 0; j < TNQ; ++j) acc[a][b][i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+  bf16x8_t af[TMQ][2], bfr[TNQ][2];
 
   auto read_a = [&](int buf, int h) {
-    const char* s = smem + buf * BUF + h * HALF + a_row;
+    const char* s = smem + buf * BUF + h * AH + a_row;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < TMQ; ++i) {
       af[i][0] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw0);
       af[i][1] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw1);
     }
   };
   auto read_b = [&](int buf, int h) {
-    const char* s = smem + buf * BUF + (2 + h) * HALF + b_row;
+    const char* s = smem + buf * BUF + 2 * AH + h * BH + b_row;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TNQ; ++j) {
       bfr[j][0] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw0);
       bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw1);
     }
   };
-  auto mma = [&](f32x4_t (&c)[4][2]) {
+  auto mma = [&](f32x4_t (&c)[TMQ][TNQ]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TMQ; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TNQ; ++j)
           c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
@@ -223,8 +241,9 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     if (more) stage_b(1, nxt);
     BAR();
     mma(acc[1][1]);
-    // A0(k+1), B0(k+1) are read in the next tile's phase 0
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // A0(k+1), B0(k+1) are read in the next tile's phase 0 (B1(k+1)'s pieces may stay in flight)
+    if (NBP % 8 == 0 || nbw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     BAR();
     // phase 3: quadrant (1,0); stage A1(k+1)
     read_b(cur, 0);
@@ -239,19 +258,20 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   BAR();
 
-  // ---- epilogue: per quadrant, the wave's 64 x 32 accumulators -> private LDS slab -> 8-column
-  // row chunks (16-byte coalesced epilogue loads / stores). (Storing straight from the fragments,
-  // 8 bytes per lane across 16 rows, measured up to 1.7x slower on the small-K shapes.)
-  constexpr int EPI_LD = 36;                    // fp32 stride of a wave's 64 x 32 slab
-  float* et = reinterpret_cast<float*>(smem) + wave * (64 * EPI_LD);
+  // ---- epilogue: per quadrant, the wave's (16 TMQ) x (16 TNQ) accumulators -> private LDS slab ->
+  // 8-column row chunks (16-byte coalesced epilogue loads / stores). (Storing straight from the
+  // fragments, 8 bytes per lane across 16 rows, measured up to 1.7x slower on the small-K shapes.)
+  constexpr int SR = TMQ * 16, SC = TNQ * 16, EPI_LD = SC + 4, CPR = SC / 8;
+  static_assert(8 * SR * EPI_LD * 4 <= 2 * BUF, "epilogue slabs");
+  float* et = reinterpret_cast<float*>(smem) + wave * (SR * EPI_LD);
   const bool geglu = p.act == 2;
   auto flush = [&](int qm, int qn) {
-    const int row0 = tile_m + qm * 128 + wr * 64;
-    const int col0 = tile_n + qn * 128 + wc * 32;
+    const int row0 = tile_m + qm * 128 + wr * SR;
+    const int col0 = tile_n + qn * (BN_ / 2) + wc * SC;
     if (geglu) {
-      // one (hidden 16 | gate 16) granule pair -> 16 outputs: 64 rows x 2 chunks
+      // BN_ = 256: one (hidden 16 | gate 16) granule pair -> 16 outputs: 64 rows x 2 chunks
 #pragma unroll 1
-      for (int ch = lane; ch < 128; ch += 64) {
+      for (int ch = lane; ch < SR * 2; ch += 64) {
         const int r = ch >> 1, oc = (ch & 1) * 8;
         if (row0 + r < p.M && col0 < p.N)
           epilogue_geglu8(p, row0 + r, col0 + oc, col0 + 16 + oc, col0 / 2 + oc, &et[r * EPI_LD + oc],
@@ -259,8 +279,8 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       }
     } else {
 #pragma unroll 1
-      for (int ch = lane; ch < 256; ch += 64) {
-        const int r = ch >> 2, c8 = (ch & 3) * 8;
+      for (int ch = lane; ch < SR * CPR; ch += 64) {
+        const int r = ch / CPR, c8 = (ch - r * CPR) * 8;
         const int ocol = col0 + c8;
         if (row0 + r < p.M && ocol < p.N) {
           float v[8];
@@ -272,11 +292,11 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       }
     }
   };
-  auto slab = [&](const f32x4_t (&c)[4][2]) {
+  auto slab = [&](const f32x4_t (&c)[TMQ][TNQ]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TMQ; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TNQ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) et[(i * 16 + fq * 4 + r) * EPI_LD + j * 16 + fr] = c[i][j][r];
   };
@@ -287,17 +307,29 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   slab(acc[1][1]); flush(1, 1);
 }
 
-int gemm8p_launch(const ActhGemmDesc* d, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes, int vec_ok,
-                  hipStream_t stream) {
+template <int BN_>
+static void launch8p(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
+                     int vec_ok, hipStream_t stream) {
+  if (d->amode == 1)
+    hipLaunchKernelGGL((gemm8p_kernel<BN_, 1>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+  else if (d->amode == 2)
+    hipLaunchKernelGGL((gemm8p_kernel<BN_, 2>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+  else
+    hipLaunchKernelGGL((gemm8p_kernel<BN_, 0>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+}
+
+// tile 4: 256 x 256; tile 5: 256 x 320 (no GEGLU: its wave column shares are not granule pairs)
+int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
+                  int vec_ok, hipStream_t stream) {
   const int mt = (d->M + 255) / 256;
   if (mt > 65535) return ACTH_EINVAL;
-  const dim3 grid((d->N + 255) / 256, mt);
-  if (d->amode == 1)
-    hipLaunchKernelGGL(gemm8p_kernel<1>, grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
-  else if (d->amode == 2)
-    hipLaunchKernelGGL(gemm8p_kernel<2>, grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
-  else
-    hipLaunchKernelGGL(gemm8p_kernel<0>, grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+  if (tile == 4) {
+    launch8p<256>(d, dim3((d->N + 255) / 256, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+  } else if (tile == 5 && d->act != 2) {
+    launch8p<320>(d, dim3((d->N + 319) / 320, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+  } else {
+    return ACTH_EINVAL;
+  }
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -19,7 +19,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 // ------------------------------------------------------------------------------------------
 
-// Flash attention v2 structure (per block: 4 waves x 32 queries, KV tiles of 64 keys):
+// Flash attention v2 structure (per block: 4 or 8 waves x 32 queries, KV tiles of 64 keys):
 //  * K and V tiles move HBM/L2 -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows per
 //    wave-instruction), double-buffered: tile j+1 is in flight while tile j is consumed; one
 //    vmcnt(0) + barrier per tile. Rows past Skv read zeros (buffer range check).
@@ -37,14 +37,18 @@ typedef __attribute__((address_space(3))) short4_t lds_short4;
 __device__ __forceinline__ int fa_swk(int key) { return (key >> 1) & 7; }
 __device__ __forceinline__ int fa_swv(int key) { return ((key >> 1) & 1) << 2; }
 
-__global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p, unsigned k_bytes, unsigned v_bytes) {
+// NW waves per block (32 queries each) share every K/V tile.
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDesc p, unsigned k_bytes,
+                                                                unsigned v_bytes) {
   __shared__ __attribute__((aligned(16))) char smem[4 * FA_TILE];   // [buf][K | V]
+  constexpr int PPW = 8 / NW;                    // DMA pieces (8 rows) per wave per tile and operand
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int h = blockIdx.y, bat = blockIdx.z;
-  const int q = blockIdx.x * 128 + wave * 32 + r32;
+  const int q = blockIdx.x * (32 * NW) + wave * 32 + r32;
   const bf16_t* qb = (const bf16_t*)p.q + bat * p.bsq + h * 64;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>((const bf16_t*)p.k + bat * p.bsk + h * 64), (short)0, (int)k_bytes, 0x00020000);
@@ -60,13 +64,13 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
     qf[s] = *reinterpret_cast<bf16x8_t*>(&t);
   }
 
-  // DMA: wave w fills rows [8w, 8w+8) and [32 + 8w, +8) of each tile; lane -> (row, physical
-  // 16-B slot lane & 7) holding logical chunk slot ^ swizzle(row)
+  // DMA: wave w fills rows [8(w + NW u), +8) of each tile; lane -> (row, physical 16-B slot
+  // lane & 7) holding logical chunk slot ^ swizzle(row)
   const int lrow = lane >> 3, slot = lane & 7;
-  int krow[2], kch[2], vch[2];
+  int krow[PPW], kch[PPW], vch[PPW];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    krow[u] = (wave + 4 * u) * 8 + lrow;
+  for (int u = 0; u < PPW; ++u) {
+    krow[u] = (wave + NW * u) * 8 + lrow;
     kch[u] = slot ^ fa_swk(krow[u]);
     vch[u] = slot ^ fa_swv(krow[u]);
   }
@@ -74,12 +78,12 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
     char* kt = smem + buf * 2 * FA_TILE;
     char* vt = kt + FA_TILE;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PPW; ++u) {
       const int key = kv0 + krow[u];
       const unsigned ko = key < p.Skv ? ((unsigned)key * p.ldk + kch[u] * 8) * 2u : 0x80000000u;
       const unsigned vo = key < p.Skv ? ((unsigned)key * p.ldv + vch[u] * 8) * 2u : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(kt + (wave + 4 * u) * 1024), 16, ko, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void*)(vt + (wave + 4 * u) * 1024), 16, vo, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(kt + (wave + NW * u) * 1024), 16, ko, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void*)(vt + (wave + NW * u) * 1024), 16, vo, 0, 0, 0);
     }
   };
 
@@ -121,24 +125,29 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
       }
     }
     // ---- online softmax (lane = query column) ----
+    // running max in log2 units: m = c * max(s) (c > 0), p = exp2(c s - m) as one FMA + v_exp
     float mx = -INFINITY;
-    const bool ragged = kv0 + 64 > p.Skv;
+    if (kv0 + 64 > p.Skv) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) st[sub][r] = -INFINITY;
+    }
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float sv = st[sub][r] * c;
-        if (ragged && kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) sv = -INFINITY;
-        st[sub][r] = sv;
-        mx = fmaxf(mx, sv);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[sub][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    m_run = m_new;
-    l_run *= alpha;
+    // rescale only when some query's max grew (otherwise every alpha is exactly 1)
+    if (__any(m_new > m_run)) {
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      l_run *= alpha;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    m_run = m_new;
 
     bf16x8_t pf[2][2];
 #pragma unroll
@@ -148,8 +157,8 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const ActhAttnDesc p
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float p0 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j] - m_new);
-          const float p1 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j + 1] - m_new);
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(st[sub][8 * s2 + 2 * j], c, -m_new));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(st[sub][8 * s2 + 2 * j + 1], c, -m_new));
           l_run += p0 + p1;
           w[j] = pack2(p0, p1);
         }
@@ -213,8 +222,13 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
   // K / V buffer extents seen from one (batch, head) base: rows x ld, minus the head offset
   const long long kb = ((long long)(d->Skv - 1) * d->ldk + 64) * 2, vb = ((long long)(d->Skv - 1) * d->ldv + 64) * 2;
   if (kb >= 0x80000000LL || vb >= 0x80000000LL) return ACTH_EINVAL;
-  dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
-  hipLaunchKernelGGL(flash_attn_kernel, grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb);
+  if (d->Sq >= 2048) {
+    dim3 grid((d->Sq + 255) / 256, d->nheads, d->nbatch);
+    hipLaunchKernelGGL(flash_attn_kernel<8>, grid, dim3(512), 0, stream, *d, (unsigned)kb, (unsigned)vb);
+  } else {
+    dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
+    hipLaunchKernelGGL(flash_attn_kernel<4>, grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb);
+  }
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -47,7 +47,8 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
 
   const int k = blockIdx.y;
   const int nc = p.nchunks;
-  const int c = blockIdx.z % nc, b = blockIdx.z / nc;
+  const int ncg = PASS == 1 ? nc - 1 : nc;       // pass 1 skips the last chunk (its end state is unused)
+  const int c = blockIdx.z % ncg, b = blockIdx.z / ncg;
   const int t = threadIdx.x;
   const int dbase = blockIdx.x * SC_THREADS;
   const int d = dbase + t;
@@ -212,9 +213,8 @@ static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
   if (d.nchunks <= 1) {
     hipLaunchKernelGGL((scan_kernel<R, 0>), dim3(gx, d.G, d.nb), dim3(SC_THREADS), 0, stream, d);
   } else {
-    ActhScanDesc d1 = d;
-    // pass 1 needs every chunk but the last; launching all keeps the grid math simple
-    hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * d.nchunks), dim3(SC_THREADS), 0, stream, d1);
+    // pass 1: every chunk but the last records its end state
+    hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * (d.nchunks - 1)), dim3(SC_THREADS), 0, stream, d);
     ACTH_CHECK_LAUNCH();
     hipLaunchKernelGGL((scan_kernel<R, 2>), dim3(gx, d.G, d.nb * d.nchunks), dim3(SC_THREADS), 0, stream, d);
   }

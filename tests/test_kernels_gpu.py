@@ -187,7 +187,7 @@ def test_conv_temporal(dev):
 
 
 # ------------------------------------------------------------------------------------------ attention
-@pytest.mark.parametrize("nb,S,heads", [(2, 64, 1), (3, 200, 2), (1, 1024, 5), (1, 144, 20)])
+@pytest.mark.parametrize("nb,S,heads", [(2, 64, 1), (3, 200, 2), (1, 1024, 5), (1, 144, 20), (1, 2304, 2), (2, 2100, 1)])
 def test_flash_attn(dev, nb, S, heads):
     C = heads * 64
     qkv = bf(rnd(nb * S, 3 * C))

@@ -37,10 +37,19 @@ typedef __attribute__((address_space(3))) short4_t lds_short4;
 __device__ __forceinline__ int fa_swk(int key) { return (key >> 1) & 7; }
 __device__ __forceinline__ int fa_swv(int key) { return ((key >> 1) & 1) << 2; }
 
+// IP-adapter epilogue (acth_ip_attn): out = vbase[ctx] + sa * ma[s] * attn + sb * mb[s] * vb[ctx]
+struct FaIpEpi {
+  const bf16_t* vbase; int ldvbase;
+  const bf16_t* vb; int ldvb;
+  const float* ma; const float* mb;
+  float sa, sb;
+  int S;
+};
+
 // NW waves per block (32 queries each) share every K/V tile.
-template <int NW>
+template <int NW, bool IP>
 __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDesc p, unsigned k_bytes,
-                                                                unsigned v_bytes) {
+                                                                unsigned v_bytes, const FaIpEpi ip) {
   __shared__ __attribute__((aligned(16))) char smem[4 * FA_TILE];   // [buf][K | V]
   constexpr int PPW = 8 / NW;                    // DMA pieces (8 rows) per wave per tile and operand
 
@@ -199,16 +208,45 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
 
   l_run += __shfl_xor(l_run, 32, 64);
   if (q >= p.Sq) return;
-  const float inv = 1.0f / l_run;
+  float inv = 1.0f / l_run;
   bf16_t* ob = (bf16_t*)p.o + bat * p.bso + (size_t)q * p.ldo + h * 64;
+  float wa = 0.0f, wb = 0.0f;
+  const bf16_t* vbr = nullptr;
+  const bf16_t* vbb = nullptr;
+  if (IP) {
+    const int s = q % ip.S;
+    inv *= ip.sa * (ip.ma ? ip.ma[s] : 1.0f);
+    vbr = ip.vbase + (size_t)bat * ip.ldvbase + h * 64;
+    if (ip.vb) {
+      wb = ip.sb * (ip.mb ? ip.mb[s] : 1.0f);
+      vbb = ip.vb + (size_t)bat * ip.ldvb + h * 64;
+    }
+  }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d0 = 8 * g + 4 * hh;
+    float a[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { a[e] = o0[4 * g + e] * inv; a[4 + e] = o1[4 * g + e] * inv; }
+    if (IP) {
+      // + vbase (+ wb * vb): 4 columns at d0 and 4 at 32 + d0
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const uint2 bw = *reinterpret_cast<const uint2*>(vbr + 32 * half + d0);
+        a[4 * half + 0] += __uint_as_float(bw.x << 16); a[4 * half + 1] += __uint_as_float(bw.x & 0xffff0000u);
+        a[4 * half + 2] += __uint_as_float(bw.y << 16); a[4 * half + 3] += __uint_as_float(bw.y & 0xffff0000u);
+        if (vbb) {
+          const uint2 cw = *reinterpret_cast<const uint2*>(vbb + 32 * half + d0);
+          a[4 * half + 0] = fmaf(wb, __uint_as_float(cw.x << 16), a[4 * half + 0]);
+          a[4 * half + 1] = fmaf(wb, __uint_as_float(cw.x & 0xffff0000u), a[4 * half + 1]);
+          a[4 * half + 2] = fmaf(wb, __uint_as_float(cw.y << 16), a[4 * half + 2]);
+          a[4 * half + 3] = fmaf(wb, __uint_as_float(cw.y & 0xffff0000u), a[4 * half + 3]);
+        }
+      }
+    }
     uint2 w0, w1;
-    w0.x = pack2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
-    w0.y = pack2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-    w1.x = pack2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
-    w1.y = pack2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    w0.x = pack2(a[0], a[1]); w0.y = pack2(a[2], a[3]);
+    w1.x = pack2(a[4], a[5]); w1.y = pack2(a[6], a[7]);
     *reinterpret_cast<uint2*>(ob + d0) = w0;
     *reinterpret_cast<uint2*>(ob + 32 + d0) = w1;
   }
@@ -222,12 +260,15 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
   // K / V buffer extents seen from one (batch, head) base: rows x ld, minus the head offset
   const long long kb = ((long long)(d->Skv - 1) * d->ldk + 64) * 2, vb = ((long long)(d->Skv - 1) * d->ldv + 64) * 2;
   if (kb >= 0x80000000LL || vb >= 0x80000000LL) return ACTH_EINVAL;
+  const FaIpEpi none = {};
   if (d->Sq >= 2048) {
     dim3 grid((d->Sq + 255) / 256, d->nheads, d->nbatch);
-    hipLaunchKernelGGL(flash_attn_kernel<8>, grid, dim3(512), 0, stream, *d, (unsigned)kb, (unsigned)vb);
+    hipLaunchKernelGGL((flash_attn_kernel<8, false>), grid, dim3(512), 0, stream, *d, (unsigned)kb, (unsigned)vb,
+                       none);
   } else {
     dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
-    hipLaunchKernelGGL(flash_attn_kernel<4>, grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb);
+    hipLaunchKernelGGL((flash_attn_kernel<4, false>), grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb,
+                       none);
   }
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
@@ -424,6 +465,36 @@ extern "C" int acth_ip_attn(const ActhIpAttnDesc* d, hipStream_t stream) {
   if (d->kv && (!d->q || d->nkeys <= 0 || d->nkeys > 32 || d->ldkv % 8 || d->ldq % 8)) return ACTH_EINVAL;
   if (d->M <= 0 || d->H <= 0 || d->rows_per_ctx <= 0 || d->S <= 0) return ACTH_EINVAL;
   if (d->ldvbase % 8 || d->ldo % 8 || (d->vb && d->ldvb % 8)) return ACTH_EINVAL;
+  if (d->kv) {
+    // the 32-key audio attention is a batched flash attention (one batch per context, one 64-key
+    // tile with keys >= nkeys masked) whose epilogue adds the ID value, the masked/scaled audio
+    // term and the VASA value
+    if (d->M % d->rows_per_ctx || d->rows_per_ctx % d->S) return ACTH_EINVAL;
+    const int C = d->H * 64;
+    ActhAttnDesc a = {};
+    a.q = d->q; a.k = d->kv; a.v = (const bf16_t*)d->kv + C; a.o = d->out;
+    a.ldq = d->ldq; a.ldk = a.ldv = d->ldkv; a.ldo = d->ldo;
+    a.bsq = (long long)d->rows_per_ctx * d->ldq;
+    a.bsk = a.bsv = (long long)d->nkeys * d->ldkv;
+    a.bso = (long long)d->rows_per_ctx * d->ldo;
+    a.nbatch = d->M / d->rows_per_ctx; a.nheads = d->H; a.Sq = d->rows_per_ctx; a.Skv = d->nkeys;
+    a.scale = d->scale;
+    if (a.nbatch > 65535 || d->H > 65535 || d->ldo % 4) return ACTH_EINVAL;
+    FaIpEpi ep;
+    ep.vbase = (const bf16_t*)d->vbase; ep.ldvbase = d->ldvbase;
+    ep.vb = (const bf16_t*)d->vb; ep.ldvb = d->ldvb;
+    ep.ma = d->mask_a; ep.mb = d->mask_b; ep.sa = d->sa; ep.sb = d->sb; ep.S = d->S;
+    const long long kb = ((long long)(d->nkeys - 1) * d->ldkv + 64) * 2;
+    if (a.Sq >= 2048) {
+      dim3 grid((a.Sq + 255) / 256, a.nheads, a.nbatch);
+      hipLaunchKernelGGL((flash_attn_kernel<8, true>), grid, dim3(512), 0, stream, a, (unsigned)kb, (unsigned)kb, ep);
+    } else {
+      dim3 grid((a.Sq + 127) / 128, a.nheads, a.nbatch);
+      hipLaunchKernelGGL((flash_attn_kernel<4, true>), grid, dim3(256), 0, stream, a, (unsigned)kb, (unsigned)kb, ep);
+    }
+    ACTH_CHECK_LAUNCH();
+    return ACTH_OK;
+  }
   const long long nblk = ((long long)d->M + 63) / 64;
   if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
   dim3 grid((unsigned)nblk, (d->H + 3) / 4);

@@ -221,31 +221,37 @@ def test_temporal_attn(dev, B, F_, S, heads):
     assert rel(out, refo) < 1e-2
 
 
-@pytest.mark.parametrize("masked", [False, True])
-def test_ip_attn(dev, masked):
-    nctx, S, heads, nk = 3, 50, 2, 32
+@pytest.mark.parametrize("masked,fps,nk,use_vb", [(False, 1, 32, True), (True, 1, 32, True), (False, 3, 7, False),
+                                                   (False, 48, 32, True)])
+def test_ip_attn(dev, masked, fps, nk, use_vb):
+    """fps = frames per context (1: spatial attn2, context = frame; >1: temporal attn2, context =
+    window, rows_per_ctx = fps * S; 48 x 50 rows exercises the 8-wave path)."""
+    nctx, S, heads = 3, 50, 2
     C = heads * 64
-    M = nctx * S
+    rpc = fps * S
+    M = nctx * rpc
     q = bf(rnd(M, C))
     kv = bf(rnd(nctx * nk, 2 * C))
     vbase = bf(rnd(nctx, C))
-    vb = bf(rnd(nctx, C))
+    vb = bf(rnd(nctx, C)) if use_vb else None
     ma = torch.rand(S) if masked else None
     mb = torch.rand(S) if masked else None
-    out = ops.ip_attn(vbase.to(dev), M, heads, S, S, q=q.to(dev), kv=kv.to(dev), nkeys=nk, vb=vb.to(dev),
-                      mask_a=None if ma is None else ma.to(dev), mask_b=None if mb is None else mb.to(dev),
-                      sa=1.25, sb=0.75)
-    qh = q.float().view(nctx, S, heads, 64).transpose(1, 2)
+    out = ops.ip_attn(vbase.to(dev), M, heads, rpc, S, q=q.to(dev), kv=kv.to(dev), nkeys=nk,
+                      vb=None if vb is None else vb.to(dev), mask_a=None if ma is None else ma.to(dev),
+                      mask_b=None if mb is None else mb.to(dev), sa=1.25, sb=0.75)
+    qh = q.float().view(nctx, rpc, heads, 64).transpose(1, 2)
     kh = kv.float()[:, :C].view(nctx, nk, heads, 64).transpose(1, 2)
     vh = kv.float()[:, C:].view(nctx, nk, heads, 64).transpose(1, 2)
-    o = F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(nctx, S, C)
-    wa = (ma if masked else torch.ones(S))[None, :, None]
-    wb = (mb if masked else torch.ones(S))[None, :, None]
-    refo = vbase.float()[:, None] + 1.25 * wa * o + 0.75 * wb * vb.float()[:, None]
+    o = F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(nctx, rpc, C)
+    wa = (ma if masked else torch.ones(S)).repeat(fps)[None, :, None]
+    refo = vbase.float()[:, None] + 1.25 * wa * o
+    if use_vb:
+        wb = (mb if masked else torch.ones(S)).repeat(fps)[None, :, None]
+        refo = refo + 0.75 * wb * vb.float()[:, None]
     assert rel(out, refo.reshape(M, C)) < 1e-2
     # 1-key-only path (no audio attention): pure broadcast
-    out2 = ops.ip_attn(vbase.to(dev), M, heads, S, S)
-    assert rel(out2, vbase.float().repeat_interleave(S, 0)) < 5e-3
+    out2 = ops.ip_attn(vbase.to(dev), M, heads, rpc, S)
+    assert rel(out2, vbase.float().repeat_interleave(rpc, 0)) < 5e-3
 
 
 # ------------------------------------------------------------------------------------------ norms

@@ -10,9 +10,10 @@
 // direction 1 visits l = L-1..0, i.e. the reference's flip_L(x) copy becomes a traversal order;
 // outputs kept for l < n_keep (selected image tokens; ID / condition tokens only feed the state).
 //
-// Parallelism. One thread owns one (b, k, d) recurrence; at ACTalker's level-0 shape that is only
-// 56*2*640 = 71,680 sequences (~1 wave per SIMD) of 9,249 serial steps, so the sequence is split
-// into nchunks chunks scanned in two passes:
+// Two kernels. scan_pair_kernel (nchunks <= 1, the default): one pass, the 16 states of a channel
+// split over a lane pair (below). scan_kernel (nchunks > 1): one thread owns one (b, k, d)
+// recurrence; at ACTalker's level-0 shape that is only 56*2*640 = 71,680 sequences (~1 wave per
+// SIMD) of 9,249 serial steps, so the sequence is split into nchunks chunks scanned in two passes:
 //   pass 1: every chunk but the last scans from h = 0 and records its end state H_c and sum(delta)_c;
 //   pass 2: chunk c folds h_in = sum_j<c ( prod_{j<i<c} exp(A*Sdelta_i) ) H_j (exact recurrence
 //           composition, 16 FMAs + exps per earlier chunk) and rescans, writing y.
@@ -207,11 +208,200 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Single-pass scan with the 16 states of a channel split over a lane pair: lane 2c + j owns
+// states [8j, 8j+8) of channel c. Twice the parallelism of one-thread-per-channel (2240 waves at
+// ACTalker's level-0 shape) without the two-pass chunk decomposition: per token a lane does half
+// of the dt_proj dot product (partner's half arrives by a DPP swap), the softplus, 8 state updates
+// and half of the C readout (summed by a second swap). Tiles of SC_T tokens of xdbl / u are staged
+// in LDS (next tile prefetched into registers); outputs are gathered per tile in LDS and stored
+// with 16-byte coalesced writes.
+#define SP_CH 128                 // channels per block (256 threads)
+
+__device__ __forceinline__ float pair_swap(float v) {
+  // value of the partner lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
+  constexpr int W = R + 32;                      // floats per token and group in xdbl
+  constexpr int R0 = (R + 1) / 2;                // dt_proj terms of lane half 0 (half 1 takes R - R0)
+  constexpr int R0P = (R0 + 3) & ~3;             // each half's dt slice, 16-byte aligned, zero padded
+  constexpr int WP = 2 * R0P + 32;               // LDS row: [dt half 0 | dt half 1 | B | C]
+  constexpr int NX = (SC_T * W + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float xs[SC_T * WP];
+  __shared__ __attribute__((aligned(16))) bf16_t us[SC_T * SP_CH];
+  __shared__ __attribute__((aligned(16))) bf16_t ys[SC_T * SP_CH];
+  __shared__ __attribute__((aligned(16))) float dls[R == 0 ? SC_T * SP_CH : 4];
+
+  const int k = blockIdx.y, b = blockIdx.z;
+  const int t = threadIdx.x;
+  const int half = t & 1, cl = t >> 1;           // state half, channel within the block
+  const int dbase = blockIdx.x * SP_CH;
+  const int d = dbase + cl;
+  const bool active = d < p.D;
+  const int dd = active ? d : 0;
+  const bool rev = (k == 1) && p.flip1;
+
+  float w[R0P > 0 ? R0P : 1];
+#pragma unroll
+  for (int r = 0; r < R0P; ++r) {
+    const int rr = half ? R0 + r : r;
+    w[r] = (r < R0 && rr < R) ? p.dt_w[((size_t)k * p.D + dd) * R + rr] : 0.0f;
+  }
+  // zero the dt padding columns once (commit() never writes them; they meet zero weights)
+  if (R > 0) {
+    for (int idx = t; idx < SC_T * 2 * R0P; idx += 256) {
+      const int tt = idx / (2 * R0P), c = idx - tt * (2 * R0P);
+      const int hf = c / R0P, r = c - hf * R0P;
+      if (r >= (hf ? R - R0 : R0)) xs[tt * WP + c] = 0.0f;
+    }
+  }
+  const float bias = p.dt_b ? p.dt_b[k * p.D + dd] : 0.0f;
+  float a2[8], h[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    a2[n] = -__expf(p.A_log[((size_t)k * p.D + dd) * 16 + 8 * half + n]) * 1.4426950408889634f;
+    h[n] = 0.0f;
+  }
+  const float dsk = p.Dskip ? p.Dskip[k * p.D + dd] : 0.0f;
+
+  const bf16_t* ub = (const bf16_t*)p.u + (size_t)b * p.L * p.ldu + (size_t)k * p.u_gstride + dbase;
+  const float* xb = p.xdbl + (size_t)b * p.L * p.ldx + k * W;
+  const size_t dl_off = (size_t)b * p.L * p.ld_delta + (size_t)k * p.D + dbase;
+  bf16_t* yb = (p.y1 && k == 1) ? (bf16_t*)p.y1 : (bf16_t*)p.y0 + (size_t)k * p.y_gstride;
+  yb += (size_t)b * p.n_keep * p.ldy + dbase;
+
+  auto pos_of = [&](int i) { return rev ? p.L - 1 - i : i; };
+  float px[NX];
+  uint4 pu;
+  float4 pd[R == 0 ? 2 : 1];
+  auto prefetch = [&](int i0) {
+#pragma unroll
+    for (int e = 0; e < NX; ++e) {
+      const int idx = t + e * 256;
+      const int tt = idx / W, col = idx - tt * W;
+      const int i = i0 + tt;
+      px[e] = (tt < SC_T && i < p.L) ? xb[(size_t)pos_of(i) * p.ldx + col] : 0.0f;
+    }
+    {
+      const int tt = t >> 4, cc = (t & 15) * 8;   // 256 x 16 B = 16 tokens x 128 channels
+      const int i = i0 + tt;
+      pu = (i < p.L && dbase + cc < p.D) ? *reinterpret_cast<const uint4*>(ub + (size_t)pos_of(i) * p.ldu + cc)
+                                         : make_uint4(0, 0, 0, 0);
+    }
+    if constexpr (R == 0) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int idx = t + e * 256;              // 512 x 4 floats = 16 tokens x 128 channels
+        const int tt = idx >> 5, cc = (idx & 31) * 4;
+        const int i = i0 + tt;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < p.L && dbase + cc < p.D) {
+          const size_t o = dl_off + (size_t)pos_of(i) * p.ld_delta + cc;
+          if (p.delta_f32) {
+            v = *reinterpret_cast<const float4*>((const float*)p.delta + o);
+          } else {
+            const uint2 r2 = *reinterpret_cast<const uint2*>((const bf16_t*)p.delta + o);
+            v = make_float4(__uint_as_float(r2.x << 16), __uint_as_float(r2.x & 0xffff0000u),
+                            __uint_as_float(r2.y << 16), __uint_as_float(r2.y & 0xffff0000u));
+          }
+        }
+        pd[e] = v;
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int e = 0; e < NX; ++e) {
+      const int idx = t + e * 256;
+      if (idx < SC_T * W) {
+        const int tt = idx / W, col = idx - tt * W;
+        const int dst = col < R0 ? col : col < R ? R0P + (col - R0) : 2 * R0P + (col - R);
+        xs[tt * WP + dst] = px[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(&us[(t >> 4) * SP_CH + (t & 15) * 8]) = pu;
+    if constexpr (R == 0) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int idx = t + e * 256;
+        *reinterpret_cast<float4*>(&dls[(idx >> 5) * SP_CH + (idx & 31) * 4]) = pd[e];
+      }
+    }
+  };
+
+  prefetch(0);
+  for (int i0 = 0; i0 < p.L; i0 += SC_T) {
+    commit();
+    __syncthreads();
+    if (i0 + SC_T < p.L) prefetch(i0 + SC_T);
+    const int nt = min(SC_T, p.L - i0);
+    // one token of the recurrence; full tiles are unrolled so the dt / exp work of later tokens
+    // (independent of h) overlaps the serial state updates
+    auto token = [&](int tt) {
+      const float* xr = xs + tt * WP;
+      float dt;
+      if constexpr (R == 0) {
+        dt = dls[tt * SP_CH + cl] + bias;
+      } else {
+        const float4* xr4 = reinterpret_cast<const float4*>(xr + half * R0P);
+        float part = 0.0f;
+#pragma unroll
+        for (int r4 = 0; r4 < R0P / 4; ++r4) {
+          const float4 v = xr4[r4];
+          part = fmaf(w[4 * r4], v.x, part);
+          part = fmaf(w[4 * r4 + 1], v.y, part);
+          part = fmaf(w[4 * r4 + 2], v.z, part);
+          part = fmaf(w[4 * r4 + 3], v.w, part);
+        }
+        dt = part + pair_swap(part) + bias;
+      }
+      if (p.softplus) dt = softplus_fast(dt);
+      const float uu = bf2f(us[tt * SP_CH + cl]);
+      const float du = dt * uu;
+      const float4* bv = reinterpret_cast<const float4*>(xr + 2 * R0P + 8 * half);
+      const float4* cv = reinterpret_cast<const float4*>(xr + 2 * R0P + 16 + 8 * half);
+      const float4 b0 = bv[0], b1 = bv[1], c0 = cv[0], c1 = cv[1];
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const float cc8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      float y = 0.0f;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        h[n] = fmaf(fast_exp2(dt * a2[n]), h[n], du * bb[n]);
+        y = fmaf(h[n], cc8[n], y);
+      }
+      y += pair_swap(y);
+      if (half == 0) ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uu, y));
+    };
+    if (nt == SC_T) {
+#pragma unroll
+      for (int tt = 0; tt < SC_T; ++tt) token(tt);
+    } else {
+      for (int tt = 0; tt < nt; ++tt) token(tt);
+    }
+    __syncthreads();
+    // coalesced store of the tile's kept outputs: 16 tokens x 128 channels, 16 B per thread
+    {
+      const int tt = t >> 4, cc = (t & 15) * 8;
+      const int i = i0 + tt;
+      if (tt < nt && dbase + cc < p.D) {
+        const int l = pos_of(i);
+        if (l < p.n_keep)
+          *reinterpret_cast<uint4*>(yb + (size_t)l * p.ldy + cc) =
+              *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
+      }
+    }
+  }
+}
+
 template <int R>
 static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
   const unsigned gx = (d.D + SC_THREADS - 1) / SC_THREADS;
   if (d.nchunks <= 1) {
-    hipLaunchKernelGGL((scan_kernel<R, 0>), dim3(gx, d.G, d.nb), dim3(SC_THREADS), 0, stream, d);
+    const unsigned gp = (d.D + SP_CH - 1) / SP_CH;
+    hipLaunchKernelGGL((scan_pair_kernel<R>), dim3(gp, d.G, d.nb), dim3(256), 0, stream, d);
   } else {
     // pass 1: every chunk but the last records its end state
     hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * (d.nchunks - 1)), dim3(SC_THREADS), 0, stream, d);

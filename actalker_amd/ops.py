@@ -316,11 +316,11 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
     return y0, y1
 
 
-def scan_auto_chunks(nb: int, G: int, D: int, L: int, target_waves: int = 8192, min_chunk: int = 128) -> int:
-    """Chunks so that (sequences / 64) * chunks >= target_waves, chunks of >= min_chunk tokens."""
-    waves = nb * G * ((D + 63) // 64)
-    want = -(-target_waves // max(waves, 1))
-    return int(max(1, min(want, L // min_chunk)))
+def scan_auto_chunks(nb: int, G: int, D: int, L: int) -> int:
+    """Single pass (the paired-lane kernel, 2 lanes per channel) at every ACTalker shape: it beats
+    the two-pass chunked kernel by 4 % / 19 % / 35 % at levels 0 / 1 / 2 (tools/bench_scan.py);
+    the chunked kernel stays available through an explicit ``nchunks`` > 1."""
+    return 1
 
 
 def _scan_chunking(d, nb, G, D, L, nchunks, device):

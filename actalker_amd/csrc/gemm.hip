@@ -194,7 +194,8 @@ static int choose_tile(const ActhGemmDesc* d) {
 
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   if (!d || !d->A || !d->B || !d->C) return ACTH_EINVAL;
-  if (d->M < 0 || d->N <= 0 || d->K <= 0) return ACTH_EINVAL;
+  // rows < 2^22: the epilogues divide row indices with a float-reciprocal estimate (udiv22)
+  if (d->M < 0 || d->M >= (1 << 22) || d->N <= 0 || d->K <= 0) return ACTH_EINVAL;
   if (d->M == 0) return ACTH_OK;
   if (d->K % 8 || d->lda % 8 || (d->A2 && (d->lda2 % 8 || d->K1 % 64)) || d->ldb % 8) return ACTH_EINVAL;
   // 16-byte epilogue vectors need 16-byte aligned rows in C / R / MIX; otherwise scalar path

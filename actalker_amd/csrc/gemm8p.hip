@@ -258,6 +258,17 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   BAR();
 
+  if (p.tile & 0x100) {                          // diagnostic: main loop only (keeps acc live)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) asm volatile("" ::"v"(acc[a][b][i][j]));
+    return;
+  }
   // ---- epilogue: per quadrant, the wave's (16 TMQ) x (16 TNQ) accumulators -> private LDS slab ->
   // 8-column row chunks (16-byte coalesced epilogue loads / stores). (Storing straight from the
   // fragments, 8 bytes per lane across 16 rows, measured up to 1.7x slower on the small-K shapes.)

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libactalker_hip.so")
+# ACTH_LIB overrides the in-tree library (A/B benchmarks of two builds in one GPU session)
+LIB_PATH = os.environ.get("ACTH_LIB") or os.path.join(_HERE, "libactalker_hip.so")
 
 c_int = ctypes.c_int
 c_float = ctypes.c_float

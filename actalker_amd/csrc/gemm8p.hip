@@ -66,6 +66,12 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   static_assert(TMQ * WR * 16 == 128 && TNQ * WC * 16 == BN_ / 2, "quadrant split");
   static_assert(2 * BUF <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  // epilogue bias / row-bias (temb) rows of this tile, staged once at kernel start so the epilogue
+  // issues no global load after its first store (vmcnt counts stores too: a load waited for after
+  // a store waits for that store's round trip)
+  constexpr int RB_IMG = 4;
+  __shared__ __attribute__((aligned(16))) float sbias[BN_];
+  __shared__ __attribute__((aligned(16))) float srb[RB_IMG * BN_];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -213,6 +219,22 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   // prologue: K tile 0 fully staged and landed
   prep_k(0);
   stage_a(0, 0); stage_b(0, 0); stage_b(1, 0); stage_a(1, 0);
+  int rb_img0 = 0, rb_nimg = 0;
+  if (p.rowbias) {
+    rb_img0 = udiv22(tile_m, p.rb_div);
+    rb_nimg = udiv22(min(p.M, tile_m + 256) - 1, p.rb_div) - rb_img0 + 1;
+  }
+  const bool rb_lds = rb_nimg <= RB_IMG;
+  for (int i = tid; i < BN_; i += 512) {
+    const int col = tile_n + i;
+    sbias[i] = (p.bias && col < p.N) ? p.bias[col] : 0.0f;
+  }
+  if (p.rowbias && rb_lds) {
+    for (int i = tid; i < rb_nimg * BN_; i += 512) {
+      const int im = i / BN_, c = i - im * BN_, col = tile_n + c;
+      srb[i] = col < p.N ? p.rowbias[(size_t)(rb_img0 + im) * p.ldrb + col] : 0.0f;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   BAR();
   if (late) BAR();
@@ -272,37 +294,14 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   // ---- epilogue: per quadrant, the wave's (16 TMQ) x (16 TNQ) accumulators -> private LDS slab ->
   // 8-column row chunks (16-byte coalesced epilogue loads / stores). (Storing straight from the
   // fragments, 8 bytes per lane across 16 rows, measured up to 1.7x slower on the small-K shapes.)
+  // Bias / row bias come from LDS (staged at kernel start): a global load waited for after a store
+  // waits for that store too (vmcnt counts both, in order), which made every chunk pay a store
+  // round trip. Measured split of the 256x320 tile at K = 320 (tools/bench_gemm.py diagnostics):
+  // main loop 53 %, slab 2 %, chunk math 16 %, stores 29 % of the kernel.
   constexpr int SR = TMQ * 16, SC = TNQ * 16, EPI_LD = SC + 4, CPR = SC / 8;
   static_assert(8 * SR * EPI_LD * 4 <= 2 * BUF, "epilogue slabs");
   float* et = reinterpret_cast<float*>(smem) + wave * (SR * EPI_LD);
   const bool geglu = p.act == 2;
-  auto flush = [&](int qm, int qn) {
-    const int row0 = tile_m + qm * 128 + wr * SR;
-    const int col0 = tile_n + qn * (BN_ / 2) + wc * SC;
-    if (geglu) {
-      // BN_ = 256: one (hidden 16 | gate 16) granule pair -> 16 outputs: 64 rows x 2 chunks
-#pragma unroll 1
-      for (int ch = lane; ch < SR * 2; ch += 64) {
-        const int r = ch >> 1, oc = (ch & 1) * 8;
-        if (row0 + r < p.M && col0 < p.N)
-          epilogue_geglu8(p, row0 + r, col0 + oc, col0 + 16 + oc, col0 / 2 + oc, &et[r * EPI_LD + oc],
-                          &et[r * EPI_LD + 16 + oc], vec_ok);
-      }
-    } else {
-#pragma unroll 1
-      for (int ch = lane; ch < SR * CPR; ch += 64) {
-        const int r = ch / CPR, c8 = (ch - r * CPR) * 8;
-        const int ocol = col0 + c8;
-        if (row0 + r < p.M && ocol < p.N) {
-          float v[8];
-          const float4 x0 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8]);
-          const float4 x1 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8 + 4]);
-          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-          epilogue8(p, row0 + r, ocol, v, vec_ok);
-        }
-      }
-    }
-  };
   auto slab = [&](const f32x4_t (&c)[TMQ][TNQ]) {
 #pragma unroll
     for (int i = 0; i < TMQ; ++i)
@@ -311,11 +310,77 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
 #pragma unroll
         for (int r = 0; r < 4; ++r) et[(i * 16 + fq * 4 + r) * EPI_LD + j * 16 + fr] = c[i][j][r];
   };
-  // the slab is private to this wave and LDS ops of one wave complete in order
-  slab(acc[0][0]); flush(0, 0);
-  slab(acc[0][1]); flush(0, 1);
-  slab(acc[1][0]); flush(1, 0);
-  slab(acc[1][1]); flush(1, 1);
+  if (geglu) {
+    // BN_ = 256: one (hidden 16 | gate 16) granule pair -> 16 outputs: SR rows x 2 chunks per quadrant
+    constexpr int NCH = SR * 2 / 64;
+    static_assert(SR * 2 % 64 == 0, "GEGLU chunks per lane");
+    auto flush_g = [&](int qm, int qn, const f32x4_t (&c)[TMQ][TNQ]) {
+      const int row0 = tile_m + qm * 128 + wr * SR;
+      const int lc0 = qn * (BN_ / 2) + wc * SC;            // tile-local first column
+      const int col0 = tile_n + lc0;
+      slab(c);
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) {
+        const int ch = lane + 64 * u;
+        const int r = ch >> 1, oc = (ch & 1) * 8;
+        if (row0 + r < p.M && col0 < p.N) {
+          float h[8], gt[8], v[8];
+          const float* hs = &et[r * EPI_LD + oc];
+          const float* gs = &et[r * EPI_LD + 16 + oc];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            h[e] = hs[e] * p.alpha + sbias[lc0 + oc + e];
+            gt[e] = gs[e] * p.alpha + sbias[lc0 + 16 + oc + e];
+            v[e] = h[e] * gelu_erf(gt[e]);
+          }
+          store8(p, out_row(p, row0 + r), col0 / 2 + oc, v, true, vec_ok);
+        }
+      }
+    };
+    flush_g(0, 0, acc[0][0]);
+    flush_g(0, 1, acc[0][1]);
+    flush_g(1, 0, acc[1][0]);
+    flush_g(1, 1, acc[1][1]);
+  } else {
+    auto flush = [&](int qm, int qn) {
+      const int row0 = tile_m + qm * 128 + wr * SR;
+      const int lc0 = qn * (BN_ / 2) + wc * SC;
+      const int col0 = tile_n + lc0;
+#pragma unroll 1
+      for (int ch = lane; ch < SR * CPR; ch += 64) {
+        const int r = ch / CPR, c8 = (ch - r * CPR) * 8;
+        const int row = row0 + r, ocol = col0 + c8;
+        if (row < p.M && ocol < p.N) {
+          float v[8];
+          const float4 x0 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8]);
+          const float4 x1 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8 + 4]);
+          const float4 b0 = *reinterpret_cast<const float4*>(&sbias[lc0 + c8]);
+          const float4 b1 = *reinterpret_cast<const float4*>(&sbias[lc0 + c8 + 4]);
+          v[0] = fmaf(x0.x, p.alpha, b0.x); v[1] = fmaf(x0.y, p.alpha, b0.y);
+          v[2] = fmaf(x0.z, p.alpha, b0.z); v[3] = fmaf(x0.w, p.alpha, b0.w);
+          v[4] = fmaf(x1.x, p.alpha, b1.x); v[5] = fmaf(x1.y, p.alpha, b1.y);
+          v[6] = fmaf(x1.z, p.alpha, b1.z); v[7] = fmaf(x1.w, p.alpha, b1.w);
+          if (p.rowbias) {
+            if (rb_lds) {
+              const float* rs = &srb[(udiv22(row, p.rb_div) - rb_img0) * BN_ + lc0 + c8];
+#pragma unroll
+              for (int k = 0; k < 8; ++k) v[k] += rs[k];
+            } else {
+              const float* rb2 = p.rowbias + (size_t)udiv22(row, p.rb_div) * p.ldrb + ocol;
+              add8(v, rb2, ocol + 8 <= p.N && !((size_t)rb2 & 15), p.N - ocol);
+            }
+          }
+          EpiPre e;
+          epi_prefetch(p, row, ocol, vec_ok, e);
+          epilogue8_tail(p, row, ocol, v, vec_ok, e);
+        }
+      }
+    };
+    slab(acc[0][0]); flush(0, 0);
+    slab(acc[0][1]); flush(0, 1);
+    slab(acc[1][0]); flush(1, 0);
+    slab(acc[1][1]); flush(1, 1);
+  }
 }
 
 template <int BN_>

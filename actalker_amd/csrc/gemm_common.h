@@ -119,6 +119,66 @@ __device__ __forceinline__ void store8(const ActhGemmDesc& p, size_t prow, int o
   }
 }
 
+// Operands of the non-GEGLU epilogue that come from HBM (residual row, AlphaBlender mix row),
+// loaded ahead of the stores that precede their use (gemm8p.hip).
+struct EpiPre { uint4 r, mix; };
+
+__device__ __forceinline__ size_t residual_row(const ActhGemmDesc& p, int row) {
+  if (!p.rmap) return (size_t)row;
+  const int q = udiv22(row, p.r_div);
+  return (size_t)p.rmap[q - udiv22(q, p.r_mod) * p.r_mod] * p.r_div + (row - q * p.r_div);
+}
+
+// 16-byte residual / mix chunks of (row, [ocol, ocol+8)) for the vector path. The loads are
+// unconditional per lane (an invalid or partial chunk reads row 0 / column 0 instead and is never
+// used), so the prefetched registers do not live across divergent branches.
+__device__ __forceinline__ void epi_prefetch(const ActhGemmDesc& p, int row, int ocol, bool ok, EpiPre& e) {
+  const bool use = ok && ocol + 8 <= p.N;
+  const int rr = use ? row : 0, cc = use ? ocol : 0;
+  if (p.R) e.r = *reinterpret_cast<const uint4*>((const bf16_t*)p.R + residual_row(p, rr) * p.ldr + cc);
+  if (p.MIX) e.mix = *reinterpret_cast<const uint4*>((const bf16_t*)p.MIX + (size_t)rr * p.ldmix + cc);
+}
+
+// Epilogue after alpha / bias / row bias: residual, SiLU / GELU, AlphaBlender mix, store. The
+// vector path takes the residual / mix chunks from e (epi_prefetch); the scalar path loads them.
+__device__ __forceinline__ void epilogue8_tail(const ActhGemmDesc& p, int row, int ocol, float* v, int vec_ok,
+                                               const EpiPre& e) {
+  const bool full = ocol + 8 <= p.N;
+  const bool vec = full && vec_ok;
+  if (p.R) {
+    float t[8];
+    if (vec) {
+      unpack8(e.r, t);
+    } else {
+      const bf16_t* rp = (const bf16_t*)p.R + residual_row(p, row) * p.ldr + ocol;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k] = (ocol + k < p.N) ? bf2f(rp[k]) : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
+  if (p.act == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = silu_f(v[k]);
+  } else if (p.act == 3) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = gelu_erf(v[k]);
+  }
+  if (p.MIX) {
+    float t[8];
+    if (vec) {
+      unpack8(e.mix, t);
+    } else {
+      const bf16_t* mp = (const bf16_t*)p.MIX + (size_t)row * p.ldmix + ocol;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k] = (ocol + k < p.N) ? bf2f(mp[k]) : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p.mix_alpha * t[k] + (1.0f - p.mix_alpha) * v[k];
+  }
+  store8(p, out_row(p, row), ocol, v, full, vec_ok);
+}
+
 // Non-GEGLU epilogue of 8 consecutive output columns [ocol, ocol+8) of output row `row`;
 // v holds the raw accumulators. Applies alpha, bias, row bias, residual (row-remapped),
 // SiLU / GELU, AlphaBlender mix, and stores (16-byte vectors when aligned).

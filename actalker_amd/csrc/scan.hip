@@ -216,20 +216,23 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
 // and half of the C readout (summed by a second swap). Tiles of SC_T tokens of xdbl / u are staged
 // in LDS (next tile prefetched into registers); outputs are gathered per tile in LDS and stored
 // with 16-byte coalesced writes.
-#define SP_CH 128                 // channels per block (256 threads)
 
 __device__ __forceinline__ float pair_swap(float v) {
   // value of the partner lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
 }
 
-template <int R>
-__global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
+// CH channels per block (2 CH threads).
+template <int R, int CH, bool SOFTPLUS>
+__global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p) {
+  constexpr int NT = 2 * CH;                     // threads
+  constexpr int SP_CH = CH;
+  constexpr int U16 = CH / 8;                    // 16-byte chunks per token row of the u / y tile
   constexpr int W = R + 32;                      // floats per token and group in xdbl
   constexpr int R0 = (R + 1) / 2;                // dt_proj terms of lane half 0 (half 1 takes R - R0)
   constexpr int R0P = (R0 + 3) & ~3;             // each half's dt slice, 16-byte aligned, zero padded
   constexpr int WP = 2 * R0P + 32;               // LDS row: [dt half 0 | dt half 1 | B | C]
-  constexpr int NX = (SC_T * W + 255) / 256;
+  constexpr int NX = (SC_T * W + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) float xs[SC_T * WP];
   __shared__ __attribute__((aligned(16))) bf16_t us[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) bf16_t ys[SC_T * SP_CH];
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
   }
   // zero the dt padding columns once (commit() never writes them; they meet zero weights)
   if (R > 0) {
-    for (int idx = t; idx < SC_T * 2 * R0P; idx += 256) {
+    for (int idx = t; idx < SC_T * 2 * R0P; idx += NT) {
       const int tt = idx / (2 * R0P), c = idx - tt * (2 * R0P);
       const int hf = c / R0P, r = c - hf * R0P;
       if (r >= (hf ? R - R0 : R0)) xs[tt * WP + c] = 0.0f;
@@ -280,13 +283,13 @@ __global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
   auto prefetch = [&](int i0) {
 #pragma unroll
     for (int e = 0; e < NX; ++e) {
-      const int idx = t + e * 256;
+      const int idx = t + e * NT;
       const int tt = idx / W, col = idx - tt * W;
       const int i = i0 + tt;
       px[e] = (tt < SC_T && i < p.L) ? xb[(size_t)pos_of(i) * p.ldx + col] : 0.0f;
     }
     {
-      const int tt = t >> 4, cc = (t & 15) * 8;   // 256 x 16 B = 16 tokens x 128 channels
+      const int tt = t / U16, cc = (t % U16) * 8;   // NT x 16 B = 16 tokens x CH channels
       const int i = i0 + tt;
       pu = (i < p.L && dbase + cc < p.D) ? *reinterpret_cast<const uint4*>(ub + (size_t)pos_of(i) * p.ldu + cc)
                                          : make_uint4(0, 0, 0, 0);
@@ -294,8 +297,8 @@ __global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
     if constexpr (R == 0) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const int idx = t + e * 256;              // 512 x 4 floats = 16 tokens x 128 channels
-        const int tt = idx >> 5, cc = (idx & 31) * 4;
+        const int idx = t + e * NT;              // 512 x 4 floats = 16 tokens x 128 channels
+        const int tt = idx / (CH / 4), cc = (idx % (CH / 4)) * 4;
         const int i = i0 + tt;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < p.L && dbase + cc < p.D) {
@@ -315,19 +318,19 @@ __global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
   auto commit = [&]() {
 #pragma unroll
     for (int e = 0; e < NX; ++e) {
-      const int idx = t + e * 256;
+      const int idx = t + e * NT;
       if (idx < SC_T * W) {
         const int tt = idx / W, col = idx - tt * W;
         const int dst = col < R0 ? col : col < R ? R0P + (col - R0) : 2 * R0P + (col - R);
         xs[tt * WP + dst] = px[e];
       }
     }
-    *reinterpret_cast<uint4*>(&us[(t >> 4) * SP_CH + (t & 15) * 8]) = pu;
+    *reinterpret_cast<uint4*>(&us[(t / U16) * SP_CH + (t % U16) * 8]) = pu;
     if constexpr (R == 0) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const int idx = t + e * 256;
-        *reinterpret_cast<float4*>(&dls[(idx >> 5) * SP_CH + (idx & 31) * 4]) = pd[e];
+        const int idx = t + e * NT;
+        *reinterpret_cast<float4*>(&dls[(idx / (CH / 4)) * SP_CH + (idx % (CH / 4)) * 4]) = pd[e];
       }
     }
   };
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
         }
         dt = part + pair_swap(part) + bias;
       }
-      if (p.softplus) dt = softplus_fast(dt);
+      if (SOFTPLUS) dt = softplus_fast(dt);
       const float uu = bf2f(us[tt * SP_CH + cl]);
       const float du = dt * uu;
       const float4* bv = reinterpret_cast<const float4*>(xr + 2 * R0P + 8 * half);
@@ -382,9 +385,9 @@ __global__ __launch_bounds__(256) void scan_pair_kernel(const ActhScanDesc p) {
       for (int tt = 0; tt < nt; ++tt) token(tt);
     }
     __syncthreads();
-    // coalesced store of the tile's kept outputs: 16 tokens x 128 channels, 16 B per thread
+    // coalesced store of the tile's kept outputs: 16 tokens x CH channels, 16 B per thread
     {
-      const int tt = t >> 4, cc = (t & 15) * 8;
+      const int tt = t / U16, cc = (t % U16) * 8;
       const int i = i0 + tt;
       if (tt < nt && dbase + cc < p.D) {
         const int l = pos_of(i);
@@ -400,8 +403,13 @@ template <int R>
 static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
   const unsigned gx = (d.D + SC_THREADS - 1) / SC_THREADS;
   if (d.nchunks <= 1) {
-    const unsigned gp = (d.D + SP_CH - 1) / SP_CH;
-    hipLaunchKernelGGL((scan_pair_kernel<R>), dim3(gp, d.G, d.nb), dim3(256), 0, stream, d);
+    // paired-lane single pass, 128 channels per block. (Measured alternatives, tools/bench_scan.py:
+    // 32-channel one-wave blocks +2 % / +22 % / +22 % at levels 0 / 1 / 2; the 16 states split over
+    // two waves with the xdbl row in SGPRs via scalar loads 1.9-3.2x slower, each token waiting
+    // on its scalar loads.)
+    const dim3 grid((d.D + 127) / 128, d.G, d.nb);
+    if (d.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true>), grid, dim3(256), 0, stream, d);
+    else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false>), grid, dim3(256), 0, stream, d);
   } else {
     // pass 1: every chunk but the last records its end state
     hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * (d.nchunks - 1)), dim3(SC_THREADS), 0, stream, d);

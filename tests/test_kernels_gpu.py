@@ -320,8 +320,10 @@ def _scan_case(nb, L, D, R, n_keep, g):
 
 @pytest.mark.parametrize("nb,L,D,R,n_keep,nchunks", [
     (2, 40, 64, 4, 30, 1), (2, 40, 64, 4, 30, 3), (1, 300, 640, 20, 267, 1), (1, 300, 640, 20, 267, 5),
-    (2, 97, 1280, 40, 64, 2), (1, 33, 2560, 80, 0, None), (3, 17, 128, 80, 17, 2), (1, 1000, 128, 20, 968, None)])
+    (2, 97, 1280, 40, 64, 2), (1, 33, 2560, 80, 0, None), (3, 17, 128, 80, 17, 2), (1, 1000, 128, 20, 968, None),
+    (2, 50, 72, 5, 40, 1), (3, 61, 200, 8, 61, 1)])
 def test_selective_scan_fused(dev, nb, L, D, R, n_keep, nchunks):
+    """nchunks: 1/None paired-lane single pass, > 1 two-pass chunked."""
     g = torch.Generator().manual_seed(nb * 1000 + L)
     u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
     xdbl = u.float() @ bf(xproj).float().t()                        # (nb*L, 2*(R+32))

@@ -21,7 +21,7 @@ SHAPES = [
 ]
 
 
-def run(mode, M, N, K, act, tile, iters, dev):
+def run(mode, M, N, K, act, tile, iters, dev, sink=False):
     g = torch.Generator(device="cpu").manual_seed(0)
     kw = {}
     if mode == "conv":
@@ -38,6 +38,9 @@ def run(mode, M, N, K, act, tile, iters, dev):
         a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)
     bias = torch.randn(N, generator=g).to(dev)
+    if sink:   # every row block writes the same 256 output rows (L2-resident): no HBM write traffic
+        kw["out"] = torch.empty(256, N // 2 if act == 2 else N, device=dev, dtype=torch.bfloat16)
+        kw["orow"] = (256, 0, 0)
     try:
         ops.gemm(a, w, bias=bias, act=act, tile=tile, **kw)
     except Exception as e:  # noqa: BLE001
@@ -58,14 +61,19 @@ def main():
     ap.add_argument("--tiles", default="0,1,2,3")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--flags", type=int, default=0, help="OR-ed into tile (0x100: skip epilogue)")
+    ap.add_argument("--only", default="", help="comma-separated SHAPES indices")
+    ap.add_argument("--sink", action="store_true", help="write all output row blocks to one 256-row buffer")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     tiles = [int(t) for t in args.tiles.split(",")]
     print("mode      M       N     K    act " + " ".join(f"tile{t:d}(TF/s)" for t in tiles), flush=True)
-    for (mode, M, N, K, act) in SHAPES:
+    only = {int(i) for i in args.only.split(",")} if args.only else None
+    for idx, (mode, M, N, K, act) in enumerate(SHAPES):
+        if only is not None and idx not in only:
+            continue
         cells = []
         for t in tiles:
-            tf, ms = run(mode, M, N, K, act, t | args.flags, args.iters, dev)
+            tf, ms = run(mode, M, N, K, act, t | args.flags, args.iters, dev, args.sink)
             cells.append(f"{tf:12.1f}" if tf is not None else f"{'n/a':>12s}")
         print(f"{mode:8s} {M:7d} {N:5d} {K:5d} {act:3d} " + " ".join(cells), flush=True)
 

@@ -1,6 +1,6 @@
 """Micro-benchmark of the fused bidirectional selective scan at the UNet's level shapes.
 
-  python tools/bench_scan.py          # single-pass paired-lane kernel vs two-pass chunked kernel
+  python tools/bench_scan.py          # paired-lane single pass vs two-pass chunked kernels
 """
 import os
 import sys
@@ -26,7 +26,8 @@ def main(iters=3):
         Dp = torch.ones(2 * D).to(dev)
         n_keep = L - 33
         res = {}
-        for nc in (1, None):
+        variants = [("pair", 1), ("chunk2", 2), ("chunk4", 4)]
+        for name, nc in variants:
             args = dict(nb=nb, L=L, R=R, n_keep=n_keep, nchunks=nc)
             y = ops.selective_scan(u, xdbl, dtw, dtb, alog, Dp, **args)
             torch.cuda.synchronize()
@@ -36,11 +37,14 @@ def main(iters=3):
                 ops.selective_scan(u, xdbl, dtw, dtb, alog, Dp, **args)
             e1.record()
             torch.cuda.synchronize()
-            res[nc] = (e0.elapsed_time(e1) / iters, y)
-        err = max(((res[1][1][i].float() - res[None][1][i].float()).norm() / res[None][1][i].float().norm()).item()
-                  for i in range(2))
-        print(f"scan nb={nb} L={L} D={D} R={R}: pair {res[1][0]:.3f} ms  two-pass {res[None][0]:.3f} ms  "
-              f"rel diff {err:.2e}", flush=True)
+            res[name] = (e0.elapsed_time(e1) / iters, y)
+        ref = res["pair"][1]
+        cells = []
+        for name, _ in variants:
+            err = max(((res[name][1][i].float() - ref[i].float()).norm() / ref[i].float().norm()).item()
+                      for i in range(2))
+            cells.append(f"{name} {res[name][0]:.3f} ms (d {err:.1e})")
+        print(f"scan nb={nb} L={L} D={D} R={R}: " + "  ".join(cells), flush=True)
 
 
 if __name__ == "__main__":

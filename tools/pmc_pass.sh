@@ -1,0 +1,11 @@
+#!/bin/bash
+# HBM traffic counters for one short bench run: FETCH_SIZE and WRITE_SIZE in separate passes
+# (they do not fit one pass on gfx950). Usage: tools/pmc_pass.sh <outdir> [bench args]
+set -o pipefail
+OUT=${1:-gpurun_out/pmc}; shift
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 240 rocprofv3 --pmc $C -f csv -d "$OUT/$C" -o run -- \
+      python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-roofline "$@" > "$OUT/$C.log" 2>&1 || exit $?
+done

@@ -278,9 +278,9 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
 // Temporal self-attention over frames. qkv rows are tokens (b, f, s) = (b*F + f)*S + s with
 // [q | k | v] column blocks of width C = H*64. Output o rows use the same token order.
 
-#define TA_TUPLES 16
+#define TA_TUPLES 8     // 8 tuples x 16 query frames = 128 threads, 32 KB of K / V: 5 blocks per CU
 
-__global__ __launch_bounds__(256) void temporal_attn_kernel(const ActhTemporalAttnDesc p) {
+__global__ __launch_bounds__(TA_TUPLES * 16) void temporal_attn_kernel(const ActhTemporalAttnDesc p) {
   __shared__ __attribute__((aligned(16))) bf16_t sk[TA_TUPLES][16][64];
   __shared__ __attribute__((aligned(16))) bf16_t sv[TA_TUPLES][16][64];
   const int tid = threadIdx.x;
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void temporal_attn_kernel(const ActhTemporalAt
   const int C = p.H * 64;
 
   // stage K and V rows: tuple tl, frame f, chunk kc
-  for (int idx = tid; idx < TA_TUPLES * 16 * 8; idx += 256) {
+  for (int idx = tid; idx < TA_TUPLES * 16 * 8; idx += TA_TUPLES * 16) {
     const int kc = idx & 7, f = (idx >> 3) & 15, tl = idx >> 7;
     const long long tp = tup0 + tl;
     uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
@@ -374,7 +374,7 @@ extern "C" int acth_temporal_attn(const ActhTemporalAttnDesc* d, hipStream_t str
   const long long ntup = (long long)d->B * d->S * d->H;
   const long long nblk = (ntup + TA_TUPLES - 1) / TA_TUPLES;
   if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
-  hipLaunchKernelGGL(temporal_attn_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  hipLaunchKernelGGL(temporal_attn_kernel, dim3((unsigned)nblk), dim3(TA_TUPLES * 16), 0, stream, *d);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -353,65 +353,95 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
 // Mamba combine + LayerNorm. Per branch: mode 0 = nothing selected (row of x), 1 = every
 // token selected in order (scan row b*L + s), 2 = position map pos[s] (-1 = unselected).
 
-__device__ __forceinline__ void mc_branch(const void* x, int ldx, const void* y0, const void* y1, int ldyy,
-                                          int L, const int* pos, int mode, long long row, int S, int ch,
-                                          float* v) {
+// Layout: LPR lanes per row (16 / 32 / 64 by width), so a wave combines 64 / LPR rows at once and
+// every lane has up to CPL 16-byte chunks of each source in flight before the first use (the
+// one-row-per-wave form it replaces ran at ~1.1 TB/s: one latency round trip per row).
+// Row reductions are xor-shuffles inside the row's lane group.
+__device__ __forceinline__ const bf16_t* mc_src(const void* x, int ldx, const void* y0, const void* y1, int ldyy,
+                                                int L, const int* pos, int mode, long long row, int S,
+                                                const bf16_t** second) {
   const long long b = row / S;
   const int s = (int)(row - b * S);
   int j = -1;
   if (mode == 1) j = s;
   else if (mode == 2) j = pos[s];
   if (j < 0) {
-    unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)x + row * ldx + ch * 8), v);
-  } else {
-    const long long r = b * L + j;
-    float a[8], c[8];
-    unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)y0 + r * ldyy + ch * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)y1 + r * ldyy + ch * 8), c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = a[e] + c[e];
+    *second = nullptr;
+    return (const bf16_t*)x + row * ldx;
   }
+  const long long r = b * L + j;
+  *second = (const bf16_t*)y1 + r * ldyy;
+  return (const bf16_t*)y0 + r * ldyy;
 }
 
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int LPR, int CPL>
 __global__ __launch_bounds__(256) void mamba_combine_kernel(const ActhMambaCombineDesc p) {
+  constexpr int RPW = 64 / LPR;                  // rows per wave
   const int lane = threadIdx.x & 63;
-  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= p.M) return;
+  const int sub = lane / LPR, gl = lane % LPR;
+  const long long row = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
+  const bool ok = row < p.M;
+  const long long rw = ok ? row : 0;
   const int nch = p.C >> 3;
-  float v[MAXCH][8];
+  const bf16_t *a0, *a1, *e0, *e1;
+  a0 = mc_src(p.xa, p.ldxa, p.ya0, p.ya1, p.ldya, p.La, p.pos_a, p.mode_a, rw, p.S, &a1);
+  e0 = mc_src(p.xe, p.ldxe, p.ye0, p.ye1, p.ldye, p.Le, p.pos_e, p.mode_e, rw, p.S, &e1);
+  uint4 ra0[CPL], ra1[CPL], re0[CPL], re1[CPL];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int ch = gl + LPR * i;
+    const bool c_ok = ok && ch < nch;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    ra0[i] = c_ok ? *reinterpret_cast<const uint4*>(a0 + ch * 8) : z;
+    ra1[i] = (c_ok && a1) ? *reinterpret_cast<const uint4*>(a1 + ch * 8) : z;
+    re0[i] = c_ok ? *reinterpret_cast<const uint4*>(e0 + ch * 8) : z;
+    re1[i] = (c_ok && e1) ? *reinterpret_cast<const uint4*>(e1 + ch * 8) : z;
+  }
+  float v[CPL][8];
   float s = 0.0f;
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int ch = lane + 64 * i;
-    if (ch < nch) {
-      float a[8], e2[8];
-      mc_branch(p.xa, p.ldxa, p.ya0, p.ya1, p.ldya, p.La, p.pos_a, p.mode_a, row, p.S, ch, a);
-      mc_branch(p.xe, p.ldxe, p.ye0, p.ye1, p.ldye, p.Le, p.pos_e, p.mode_e, row, p.S, ch, e2);
+  for (int i = 0; i < CPL; ++i) {
+    float t0[8], t1[8], t2[8], t3[8];
+    unpack8(ra0[i], t0); unpack8(ra1[i], t1); unpack8(re0[i], t2); unpack8(re1[i], t3);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { v[i][e] = a[e] + e2[e]; s += v[i][e]; }
+    for (int e = 0; e < 8; ++e) {
+      // (y0 + y1) + (x or y0' + y1'): a branch's two scan directions are summed first, as in
+      // the reference's y = out[:, 0] + flip(out[:, 1]) before the cross-branch add
+      v[i][e] = (t0[e] + t1[e]) + (t2[e] + t3[e]);
+      s += v[i][e];
     }
   }
-  const float mean = wave_sum(s) / p.C;
+  const float mean = group_sum<LPR>(s) / p.C;
   float q = 0.0f;
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int ch = lane + 64 * i;
-    if (ch < nch) {
+  for (int i = 0; i < CPL; ++i) {
+    if (gl + LPR * i < nch) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; q += d * d; }
     }
   }
-  const float rstd = rsqrtf(wave_sum(q) / p.C + p.eps);
+  const float rstd = rsqrtf(group_sum<LPR>(q) / p.C + p.eps);
+  if (!ok) return;
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int ch = lane + 64 * i;
+  for (int i = 0; i < CPL; ++i) {
+    const int ch = gl + LPR * i;
     if (ch < nch) {
+      const float4 g0 = *reinterpret_cast<const float4*>(p.gamma + ch * 8);
+      const float4 g1 = *reinterpret_cast<const float4*>(p.gamma + ch * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(p.beta + ch * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.beta + ch * 8 + 4);
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       float o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = ch * 8 + e;
-        o[e] = (v[i][e] - mean) * rstd * p.gamma[c] + p.beta[c];
-      }
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + bb[e];
       *reinterpret_cast<uint4*>((bf16_t*)p.y + row * p.ldy + ch * 8) = pack8(o);
     }
   }
@@ -419,7 +449,8 @@ __global__ __launch_bounds__(256) void mamba_combine_kernel(const ActhMambaCombi
 
 extern "C" int acth_mamba_combine_ln(const ActhMambaCombineDesc* d, hipStream_t stream) {
   if (!d || !d->y || !d->gamma || !d->beta) return ACTH_EINVAL;
-  if (d->C % 8 || d->C > 64 * 8 * MAXCH || d->S <= 0 || d->M % d->S) return ACTH_EINVAL;
+  if (d->C % 8 || d->C > 64 * 8 * 6 || d->S <= 0 || d->M % d->S) return ACTH_EINVAL;
+  if (((size_t)d->gamma | (size_t)d->beta) & 15) return ACTH_EINVAL;
   const int modes[2] = {d->mode_a, d->mode_e};
   const void* xs[2] = {d->xa, d->xe};
   const void* ys[2] = {d->ya0, d->ye0};
@@ -432,8 +463,19 @@ extern "C" int acth_mamba_combine_ln(const ActhMambaCombineDesc* d, hipStream_t 
     if (modes[i] == 2 && !ps[i]) return ACTH_EINVAL;
   }
   if (d->M == 0) return ACTH_OK;
-  const long long nblk = ((long long)d->M + 3) / 4;
-  hipLaunchKernelGGL(mamba_combine_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  const int nch = d->C / 8;
+  // lanes per row: the smallest group that keeps a lane at <= 6 chunks per source
+  const int lpr = nch <= 16 * 6 ? 16 : nch <= 32 * 6 ? 32 : 64;
+  const long long rows_per_blk = 4LL * (64 / lpr);
+  const unsigned nblk = (unsigned)((d->M + rows_per_blk - 1) / rows_per_blk);
+  if (lpr == 16) {
+    if (nch <= 16 * 2) hipLaunchKernelGGL((mamba_combine_kernel<16, 2>), dim3(nblk), dim3(256), 0, stream, *d);
+    else hipLaunchKernelGGL((mamba_combine_kernel<16, 6>), dim3(nblk), dim3(256), 0, stream, *d);
+  } else if (lpr == 32) {
+    hipLaunchKernelGGL((mamba_combine_kernel<32, 6>), dim3(nblk), dim3(256), 0, stream, *d);
+  } else {
+    hipLaunchKernelGGL((mamba_combine_kernel<64, 6>), dim3(nblk), dim3(256), 0, stream, *d);
+  }
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

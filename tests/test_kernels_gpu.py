@@ -96,7 +96,8 @@ def test_gemm_geglu_and_orow(dev):
 
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
 def test_gemm_tile_variants(dev, tile):
-    """Every tile kernel (128x128; 256x256 and 256x160 8-wave) on all A loaders, tails and epilogues."""
+    """Every tile kernel (128x128; 256x256 / 256x160 8-wave; phased 256x256 / 256x320) on all A
+    loaders, tails and epilogues."""
     from actalker_amd.modules import pack_conv3x3, pack_conv3d_t, pack_geglu
     # dense, ragged M/N/K + bias + residual + silu, fp32 out
     M, N, K = 700, 330, 200
@@ -115,6 +116,10 @@ def test_gemm_tile_variants(dev, tile):
                    mix_alpha=0.25, tile=tile)
     base = torch.cat([a1, a2], 1).float() @ w2.float().t() + rowb.repeat_interleave(350, 0)
     assert rel(out, 0.25 * mix.float() + 0.75 * base) < 1e-2
+    # row bias changing every 100 rows (more images per row tile than the LDS-staged kernels hold)
+    rowb7 = rnd(7, N)
+    out = ops.gemm(a.to(dev), w.to(dev), rowbias=rowb7.to(dev), rb_div=100, tile=tile)
+    assert rel(out, a.float() @ w.float().t() + rowb7.repeat_interleave(100, 0)) < 1e-2
     # conv3x3 with skip concat, stride 1 / 2 / upsample
     B, H, W, C1, C2, Co = 2, 12, 20, 128, 64, 320
     x1, x2 = bf(rnd(B, C1, H, W)), bf(rnd(B, C2, H, W))

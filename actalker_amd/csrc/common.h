@@ -56,8 +56,13 @@ __device__ __forceinline__ void unpack8(const uint4 v, float* f) {
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
 }
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// two floats -> packed bf16 pair (low = a) in ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving); two
+// scalar f2bf conversions + shift + or cost three extra VALU per pair in every epilogue
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
 
 __device__ __forceinline__ uint4 pack8(const float* f) {

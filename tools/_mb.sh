@@ -1,5 +1,10 @@
 set -o pipefail
-mkdir -p gpurun_out/mb19
+mkdir -p gpurun_out/mb22
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/mb19/pytest.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mb19/prof -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/mb19/prof.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/mb22/pytest.log 2>&1 || exit 1
+for L in head pk pkstag; do
+ACTH_LIB=$PWD/ab/lib_$L.so timeout -k 10 120 python -u tools/bench_attn.py > gpurun_out/mb22/attn_$L.log 2>&1 || exit 1
+done
+for L in head pk; do
+ACTH_LIB=$PWD/ab/lib_$L.so timeout -k 10 300 python -u tools/bench_gemm.py --tiles 0 > gpurun_out/mb22/gemm_$L.log 2>&1 || exit 1
+done

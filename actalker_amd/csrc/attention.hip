@@ -278,93 +278,102 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
 // Temporal self-attention over frames. qkv rows are tokens (b, f, s) = (b*F + f)*S + s with
 // [q | k | v] column blocks of width C = H*64. Output o rows use the same token order.
 
-#define TA_TUPLES 8     // 8 tuples x 16 query frames = 128 threads, 32 KB of K / V: 5 blocks per CU
+// One wave per (b, s, head) tuple at a time, the F <= 16 frames padded to
+// one 16 x 16 tile. Per tuple a lane issues 6 16-byte loads and the wave 6 MFMAs:
+//   S^T = K Q^T  v_mfma_f32_16x16x32_bf16 x 2: A = K, B = Q^T, both loaded as 16-B row chunks
+//                (lane l -> frame l % 16, dims 32 ks + 8 (l / 16)); lane l then holds the scores of
+//                keys 4 (l / 16) + i for query l % 16, so the softmax is in-lane + xor 16 / 32.
+//   O^T = V^T P^T  v_mfma_f32_16x16x16bf16_1k x 4 (d tiles): B = P^T is the score accumulator
+//                itself (as bf16), A = V^T from a per-wave LDS transpose of the V tile.
+// (A thread-per-query VALU kernel spent ~1000 VALU wave-instructions per tuple against ~60 here; both
+// are bound by the frame-strided row reads, ~2.5 TB/s at the level-0 shape, tools/bench_attn.py.)
+#define TM_TPW 4                 // tuples per wave (consecutive: heads of one row segment)
+#define TM_VLD 20                // V^T LDS row: 16 keys + pad (40 B, 8-B aligned reads)
 
-__global__ __launch_bounds__(TA_TUPLES * 16) void temporal_attn_kernel(const ActhTemporalAttnDesc p) {
-  __shared__ __attribute__((aligned(16))) bf16_t sk[TA_TUPLES][16][64];
-  __shared__ __attribute__((aligned(16))) bf16_t sv[TA_TUPLES][16][64];
-  const int tid = threadIdx.x;
+__global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTemporalAttnDesc p) {
+  __shared__ __attribute__((aligned(16))) bf16_t vts[4][64 * TM_VLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
   const long long ntup = (long long)p.B * p.S * p.H;
-  const long long tup0 = (long long)blockIdx.x * TA_TUPLES;
   const int C = p.H * 64;
-
-  // stage K and V rows: tuple tl, frame f, chunk kc
-  for (int idx = tid; idx < TA_TUPLES * 16 * 8; idx += TA_TUPLES * 16) {
-    const int kc = idx & 7, f = (idx >> 3) & 15, tl = idx >> 7;
-    const long long tp = tup0 + tl;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (tp < ntup && f < p.F) {
-      const int h = (int)(tp % p.H);
-      const long long bs = tp / p.H;
-      const int s = (int)(bs % p.S), b = (int)(bs / p.S);
-      const size_t row = ((size_t)b * p.F + f) * p.S + s;
-      const bf16_t* base = (const bf16_t*)p.qkv + row * p.ldqkv + h * 64 + kc * 8;
-      kv = *reinterpret_cast<const uint4*>(base + C);
-      vv = *reinterpret_cast<const uint4*>(base + 2 * C);
-    }
-    *reinterpret_cast<uint4*>(&sk[tl][f][kc * 8]) = kv;
-    *reinterpret_cast<uint4*>(&sv[tl][f][kc * 8]) = vv;
-  }
-  __syncthreads();
-
-  const int tl = tid >> 4, fq = tid & 15;
-  const long long tp = tup0 + tl;
-  if (tp >= ntup || fq >= p.F) return;
-  const int h = (int)(tp % p.H);
-  const long long bs = tp / p.H;
-  const int s = (int)(bs % p.S), b = (int)(bs / p.S);
-  const size_t row = ((size_t)b * p.F + fq) * p.S + s;
-
-  float qv[64];
-  const bf16_t* qrow = (const bf16_t*)p.qkv + row * p.ldqkv + h * 64;
+  const float c = p.scale * 1.4426950408889634f;
+  bf16_t* vt = vts[wave];
+  const bool fok = fr < p.F;
+  // every load of the wave's TM_TPW tuples is issued before the first is used (one latency per
+  // wave instead of one per tuple: the rows of a tuple are S rows apart, 64 B per lane group)
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  uint4 qa[TM_TPW][2], ka[TM_TPW][2], va[TM_TPW][2];
+  size_t rows[TM_TPW];
+  int heads[TM_TPW];
+  const long long tp0 = ((long long)blockIdx.x * 4 + wave) * TM_TPW;
 #pragma unroll
-  for (int cc = 0; cc < 8; ++cc) unpack8(*reinterpret_cast<const uint4*>(qrow + cc * 8), qv + cc * 8);
-
-  float sc[16];
-  float mx = -INFINITY;
+  for (int it = 0; it < TM_TPW; ++it) {
+    const long long tp = tp0 + it < ntup ? tp0 + it : ntup - 1;
+    const int h = (int)(tp % p.H);
+    const long long bs = tp / p.H;
+    const int s = (int)(bs % p.S), b = (int)(bs / p.S);
+    rows[it] = ((size_t)b * p.F + (fok ? fr : 0)) * p.S + s;           // frame fr of this tuple
+    heads[it] = h;
+    const bf16_t* base = (const bf16_t*)p.qkv + rows[it] * p.ldqkv + h * 64 + 8 * g;
 #pragma unroll
-  for (int fk = 0; fk < 16; ++fk) {
-    float acc = 0.0f;
-    if (fk < p.F) {
-#pragma unroll
-      for (int cc = 0; cc < 8; ++cc) {
-        float kf[8];
-        unpack8(*reinterpret_cast<const uint4*>(&sk[tl][fk][cc * 8]), kf);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc = fmaf(qv[cc * 8 + e], kf[e], acc);
-      }
-      acc *= p.scale;
-      mx = fmaxf(mx, acc);
-    }
-    sc[fk] = acc;
-  }
-  float den = 0.0f;
-#pragma unroll
-  for (int fk = 0; fk < 16; ++fk) {
-    const float e = fk < p.F ? __expf(sc[fk] - mx) : 0.0f;
-    sc[fk] = e;
-    den += e;
-  }
-  const float inv = 1.0f / den;
-  float ov[64];
-#pragma unroll
-  for (int d = 0; d < 64; ++d) ov[d] = 0.0f;
-#pragma unroll
-  for (int fk = 0; fk < 16; ++fk) {
-    if (fk < p.F) {
-      const float w = sc[fk] * inv;
-#pragma unroll
-      for (int cc = 0; cc < 8; ++cc) {
-        float vf[8];
-        unpack8(*reinterpret_cast<const uint4*>(&sv[tl][fk][cc * 8]), vf);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ov[cc * 8 + e] = fmaf(w, vf[e], ov[cc * 8 + e]);
-      }
+    for (int ks = 0; ks < 2; ++ks) {
+      qa[it][ks] = fok ? *reinterpret_cast<const uint4*>(base + 32 * ks) : z;
+      ka[it][ks] = fok ? *reinterpret_cast<const uint4*>(base + C + 32 * ks) : z;
+      va[it][ks] = fok ? *reinterpret_cast<const uint4*>(base + 2 * C + 32 * ks) : z;
     }
   }
-  bf16_t* orow = (bf16_t*)p.o + row * p.ldo + h * 64;
 #pragma unroll
-  for (int cc = 0; cc < 8; ++cc) *reinterpret_cast<uint4*>(orow + cc * 8) = pack8(ov + cc * 8);
+  for (int it = 0; it < TM_TPW; ++it) {
+    if (tp0 + it >= ntup) break;
+    const size_t row = rows[it];
+    const int h = heads[it];
+    const uint4* qv = qa[it];
+    const uint4* kv = ka[it];
+    const uint4* vv = va[it];
+    // V^T[d][key] (lane holds V[key fr][d = 32 ks + 8 g + e]); the previous tuple's reads of vt
+    // were issued earlier by this wave, and a wave's LDS operations complete in order
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv[ks]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vt[(32 * ks + 8 * g + e) * TM_VLD + fr] = ve[e];
+    }
+    f32x4_t st = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8_t*>(&kv[ks]),
+                                                   *reinterpret_cast<const bf16x8_t*>(&qv[ks]), st, 0, 0, 0);
+    // softmax over the keys of query fr: keys 4 g + i here, the other 12 in lanes fr + 16 k
+    float sc[4], mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sc[i] = (4 * g + i < p.F) ? st[i] * c : -INFINITY;
+      mx = fmaxf(mx, sc[i]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float pr[4], sum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pr[i] = __builtin_amdgcn_exp2f(sc[i] - mx);
+      sum += pr[i];
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.0f / sum;
+    // P^T as the B operand: element j = key 4 g + j of query fr
+    const short4_t pb = __builtin_bit_cast(short4_t, make_uint2(pack2(pr[0], pr[1]), pack2(pr[2], pr[3])));
+    bf16_t* orow = (bf16_t*)p.o + row * p.ldo + h * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const short4_t a = *reinterpret_cast<const short4_t*>(&vt[(16 * dt + fr) * TM_VLD + 4 * g]);
+      const f32x4_t o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, f32x4_t{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+      // o[i] = O[query fr][d = 16 dt + 4 g + i]
+      if (fok)
+        *reinterpret_cast<uint2*>(orow + 16 * dt) =
+            make_uint2(pack2(o[0] * inv, o[1] * inv), pack2(o[2] * inv, o[3] * inv));
+    }
+  }
 }
 
 extern "C" int acth_temporal_attn(const ActhTemporalAttnDesc* d, hipStream_t stream) {
@@ -372,9 +381,9 @@ extern "C" int acth_temporal_attn(const ActhTemporalAttnDesc* d, hipStream_t str
   if (d->F <= 0 || d->F > 16 || d->B <= 0 || d->S <= 0 || d->H <= 0) return ACTH_EINVAL;
   if (d->ldqkv % 8 || d->ldo % 8) return ACTH_EINVAL;
   const long long ntup = (long long)d->B * d->S * d->H;
-  const long long nblk = (ntup + TA_TUPLES - 1) / TA_TUPLES;
+  const long long nblk = (ntup + 4 * TM_TPW - 1) / (4 * TM_TPW);
   if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
-  hipLaunchKernelGGL(temporal_attn_kernel, dim3((unsigned)nblk), dim3(TA_TUPLES * 16), 0, stream, *d);
+  hipLaunchKernelGGL(temporal_attn_mfma_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, *d);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -188,7 +188,7 @@ extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
 // GroupNorm. Rows are tokens; statistics batch = row / rows_per_stat; group = c / (C/G).
 // Input may be the channel concat of x (C1 channels) and x2 (C - C1 channels).
 
-// Statistics: each block reduces GS_ROWS rows of one statistics batch to per-channel fp32 partial
+// Statistics: each block reduces gs_rows rows of one statistics batch to per-channel fp32 partial
 // sums (LDS), folds them in a fixed order to per-group fp64 sums and adds those to fp64
 // accumulators (2*G doubles per batch; fp64 sums of fp32 partials are exact in practice, so the
 // cross-block atomics do not make the result order-dependent). Apply: each block covers rows of a single batch, turns (mean, rstd, gamma, beta) into a
@@ -196,7 +196,6 @@ extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
 // Thread layout of both: nchl = min(C/8, 256) chunk columns x (256 / nchl) row lanes; a thread
 // owns chunk columns cl and cl + nchl (C <= 4096).
 
-#define GS_ROWS 128
 
 __device__ __forceinline__ uint4 gn_load(const ActhGroupNormDesc& p, long long row, int ch) {
   const int c = ch * 8;
@@ -204,8 +203,10 @@ __device__ __forceinline__ uint4 gn_load(const ActhGroupNormDesc& p, long long r
   return *reinterpret_cast<const uint4*>((const bf16_t*)p.x2 + row * p.ldx2 + (c - p.C1));
 }
 
-// grid: (ceil(rows_per_stat / GS_ROWS), nstat)
-__global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p) {
+// grid: (ceil(rows_per_stat / gs_rows), nstat); gs_rows (rows per block) is the largest of
+// 128 / 256 / 512 that still gives >= 1024 blocks: the per-block fold below is serial, so fewer,
+// fuller blocks keep the pass streaming (128-row blocks ran at ~3.2 TB/s on the level-0 shapes)
+__global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p, int gs_rows) {
   // per row lane, per channel partial sums (written once each, reduced in a fixed order below, so
   // the statistics are bit-reproducible): rows_par * 2C <= 8192 floats for C <= 4096
   __shared__ float red[8192];
@@ -214,8 +215,8 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p
   const int rows_par = 256 / nchl;
   const int t = threadIdx.x;
   const int stat = blockIdx.y;
-  const long long r_begin = (long long)stat * p.rows_per_stat + (long long)blockIdx.x * GS_ROWS;
-  const long long r_end = min((long long)stat * p.rows_per_stat + p.rows_per_stat, r_begin + GS_ROWS);
+  const long long r_begin = (long long)stat * p.rows_per_stat + (long long)blockIdx.x * gs_rows;
+  const long long r_end = min((long long)stat * p.rows_per_stat + p.rows_per_stat, r_begin + gs_rows);
   const int rl = t / nchl, cl = t - rl * nchl;
   if (rl < rows_par) {
     for (int ch = cl; ch < nch; ch += nchl) {
@@ -339,8 +340,10 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   if (nstat > 65535) return ACTH_EINVAL;
   if (hipMemsetAsync(d->ws, 0, (size_t)nstat * d->G * 2 * sizeof(double), stream) != hipSuccess)
     return ACTH_ELAUNCH;
-  dim3 g1((d->rows_per_stat + GS_ROWS - 1) / GS_ROWS, nstat);
-  hipLaunchKernelGGL(gn_stats_kernel, g1, dim3(256), 0, stream, *d);
+  int gs_rows = 512;
+  while (gs_rows > 128 && (long long)((d->rows_per_stat + gs_rows - 1) / gs_rows) * nstat < 1024) gs_rows >>= 1;
+  dim3 g1((d->rows_per_stat + gs_rows - 1) / gs_rows, nstat);
+  hipLaunchKernelGGL(gn_stats_kernel, g1, dim3(256), 0, stream, *d, gs_rows);
   ACTH_CHECK_LAUNCH();
   int rpb = 128;
   while (d->rows_per_stat % rpb) rpb >>= 1;

@@ -88,12 +88,41 @@ def synthetic_inputs(N, fpb, H, W, mode, seed=72589):
                 masks=masks)
 
 
+def gemm_algorithmic_bytes(a, w, M, N, K, kw):
+    """HBM bytes one acth_gemm launch must move at minimum: each A source element once (an
+    implicit-conv image once, not 9x), the weights, the output, and residual / mix rows."""
+    esz = 2
+    if kw.get("conv") is not None:
+        c = kw["conv"]
+        a_elems = c["B"] * c["H"] * c["W"] * (a.shape[1] + (kw["a2"].shape[1] if kw.get("a2") is not None else 0))
+    elif kw.get("temporal") is not None:
+        a_elems = M * (a.shape[1] + (kw["a2"].shape[1] if kw.get("a2") is not None else 0))
+    else:
+        a_elems = M * K
+    n_out = N // 2 if kw.get("act", 0) == 2 else N
+    out_b = 4 if kw.get("out_f32") else 2
+    extra = (M * N * esz if kw.get("residual") is not None else 0) + (M * N * esz if kw.get("mix") is not None else 0)
+    return a_elems * esz + N * K * esz + M * n_out * out_b + extra
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the GEMM launches measured by rocprofv3 PMC passes of this command
+    (tools/pmc_pass.sh -> tools/pmc_summary.py --json -> profiles/pmc_traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh).get("acth_gemm")
+    except (OSError, ValueError):
+        return None
+
+
 class GemmTimer:
     """HIP events around every GEMM launch on the launch stream (torch's current stream)."""
 
     def __init__(self):
         self.events = []
         self.flops = 0.0
+        self.bytes = 0.0
         self.launches = 0
 
     def install(self):
@@ -117,6 +146,7 @@ class GemmTimer:
             else:
                 M = a.shape[0]
             self.flops += 2.0 * M * N * K
+            self.bytes += gemm_algorithmic_bytes(a, w, M, N, K, kw)
             self.launches += 1
             mode = "conv" if kw.get("conv") is not None else "temporal" if kw.get("temporal") is not None else "dense"
             self.events.append((e0, e1, (mode, M, N, K, kw.get("act", 0))))
@@ -251,9 +281,16 @@ def main():
         if os.environ.get("ACTH_GEMM_STATS"):
             log(timer.shape_report())
         achieved = timer.flops / (gemm_ms / 1000.0) / 1e12
+        pmc = pmc_traffic()
         roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / PEAK_BF16_TFLOPS, 4), traffic=None, kernel="gemm_bf16_kernel",
+                    frac=round(achieved / PEAK_BF16_TFLOPS, 4),
+                    traffic=(round(pmc["hbm_bytes_per_launch"]) if pmc else None),
+                    traffic_unit="bytes/launch (PMC 2*FETCH_SIZE + WRITE_SIZE)",
+                    traffic_source=(pmc or {}).get("source"),
+                    algorithmic_bytes_per_launch=round(timer.bytes / timer.launches),
+                    kernel="acth_gemm (gemm8p_kernel<320|256,A> + gemm256_kernel + gemm_bf16_kernel launches)",
                     launches=timer.launches, avg_launch_us=round(1000.0 * gemm_ms / timer.launches, 2),
+                    flop_per_launch=round(timer.flops / timer.launches),
                     kernel_share_of_step=round(gemm_ms / (elapsed * 1000.0), 3))
     n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank)[0])
     frame_fwds = n_units_rank * fpb * args.steps

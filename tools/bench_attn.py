@@ -29,6 +29,21 @@ def main(iters=5):
         ms = e0.elapsed_time(e1) / iters
         flops = 4.0 * nb * H * S * S * 64
         print(f"flash_attn nb={nb} S={S} H={H}: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s", flush=True)
+    # temporal attention over the 14 frames of a window (B = 4 CFG branches), HBM-bound
+    for S, H in ((9216, 5), (2304, 10), (576, 20)):
+        B, F = 4, 14
+        qkv = torch.randn(B * F * S, 3 * H * 64, generator=g).to(dev, torch.bfloat16)
+        ops.temporal_attn(qkv, B, F, S, H)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            ops.temporal_attn(qkv, B, F, S, H)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        nbytes = B * F * S * H * 64 * 2 * 4            # q, k, v read + o written
+        print(f"temporal_attn S={S} H={H}: {ms:.3f} ms  {nbytes / ms / 1e9:.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -30,6 +30,19 @@ def main():
         wr = 1024.0 * sum(wv)
         rows.append((name, len(fv), rd, wr))
     rows.sort(key=lambda r: -(r[2] + r[3]))
+    if "--json" in sys.argv:
+        # per-launch average over every acth_gemm kernel (names containing "gemm"), for
+        # bench.py's roofline.traffic
+        import json
+        out = sys.argv[sys.argv.index("--json") + 1]
+        src = sys.argv[sys.argv.index("--source") + 1] if "--source" in sys.argv else d
+        g = [r for r in rows if "gemm" in r[0]]
+        n = sum(r[1] for r in g)
+        with open(out, "w") as fh:
+            json.dump({"acth_gemm": {"hbm_bytes_per_launch": sum(r[2] + r[3] for r in g) / max(n, 1),
+                                     "dispatches": n, "read_bytes": sum(r[2] for r in g),
+                                     "write_bytes": sum(r[3] for r in g), "source": src}}, fh, indent=1)
+        return
     w = csv.writer(sys.stdout)
     w.writerow(["Name", "Dispatches", "ReadBytesTotal", "WriteBytesTotal", "HbmBytesPerDispatch"])
     for name, n, rd, wr in rows:

@@ -18,6 +18,9 @@ SHAPES = [
     ("dense", 129024, 640, 640, 0), ("dense", 129024, 640, 2560, 0), ("conv", 32256, 1280, 11520, 0),
     ("temporal", 516096, 320, 960, 0), ("conv", 129024, 640, 5760, 0), ("dense", 32256, 1280, 5120, 0),
     ("dense", 516096, 960, 320, 0), ("dense", 32256, 1280, 1280, 0), ("conv", 8064, 1280, 11520, 0),
+    # reference points (not UNet shapes): square 4096^3 / 8192^3 (operands L2 / MALL resident),
+    # and a 2048-wide K = 4096 panel streaming a 1 GB A from HBM
+    ("dense", 4096, 4096, 4096, 0), ("dense", 8192, 8192, 8192, 0), ("dense", 131072, 2048, 4096, 0),
 ]
 
 

@@ -218,6 +218,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--concurrent-calls", type=int, default=1,
+                    help="run a rank's independent UNet calls of a step on this many HIP streams")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -246,7 +248,8 @@ def main():
     backend = pl.HipBackend(unet, H // 8, W // 8, inp["masks"], gate, inp["added"], N + fpb, fpb,
                             inp["image_latents"], inp["image_embeddings"], inp["audio_prompts"],
                             inp["vasa_prompts"], inp["pose_fea"])
-    cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7)
+    cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7,
+                        concurrent_calls=args.concurrent_calls)
 
     def barrier():
         if world > 1:

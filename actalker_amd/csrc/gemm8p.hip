@@ -64,14 +64,17 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   constexpr int NBP = BN_ / 16;                 // DMA pieces per B half-tile
   constexpr int NBJ = (NBP + 7) / 8;
   static_assert(TMQ * WR * 16 == 128 && TNQ * WC * 16 == BN_ / 2, "quadrant split");
-  static_assert(2 * BUF <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  static_assert(2 * BUF + 5 * BN_ * 4 <= 160 * 1024, "LDS");
   // epilogue bias / row-bias (temb) rows of this tile, staged once at kernel start so the epilogue
   // issues no global load after its first store (vmcnt counts stores too: a load waited for after
-  // a store waits for that store's round trip)
+  // a store waits for that store's round trip). They live in the SAME __shared__ array as the
+  // staging buffers, past them: a second __shared__ object makes hipcc emit vmcnt(0) before every
+  // phase's ds_reads (it cannot rule out the in-flight LDS-DMA writing it), which drains the
+  // counted-vmcnt pipeline (cdna_hip_programming.md §5, "Projection GEMM" item 4(a)).
   constexpr int RB_IMG = 4;
-  __shared__ __attribute__((aligned(16))) float sbias[BN_];
-  __shared__ __attribute__((aligned(16))) float srb[RB_IMG * BN_];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + (1 + RB_IMG) * BN_ * 4];
+  float* const sbias = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* const srb = sbias + BN_;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

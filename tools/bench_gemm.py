@@ -59,17 +59,36 @@ def run(mode, M, N, K, act, tile, iters, dev, sink=False):
     return 2.0 * M * N * K / (ms / 1e3) / 1e12, ms
 
 
+def run_lib(M, N, K, iters, dev):
+    """torch.matmul (hipBLASLt) on the same dense shape, no epilogue: the library reference point."""
+    g = torch.Generator(device="cpu").manual_seed(0)
+    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)
+    torch.matmul(a, w.t())
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        torch.matmul(a, w.t())
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return 2.0 * M * N * K / (ms / 1e3) / 1e12
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="0,1,2,3")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--flags", type=int, default=0, help="OR-ed into tile (0x100: skip epilogue)")
     ap.add_argument("--only", default="", help="comma-separated SHAPES indices")
+    ap.add_argument("--lib", action="store_true", help="add a torch.matmul (hipBLASLt) column for dense shapes")
     ap.add_argument("--sink", action="store_true", help="write all output row blocks to one 256-row buffer")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     tiles = [int(t) for t in args.tiles.split(",")]
-    print("mode      M       N     K    act " + " ".join(f"tile{t:d}(TF/s)" for t in tiles), flush=True)
+    print("mode      M       N     K    act " + " ".join(f"tile{t:d}(TF/s)" for t in tiles)
+          + ("   hipblaslt" if args.lib else ""), flush=True)
     only = {int(i) for i in args.only.split(",")} if args.only else None
     for idx, (mode, M, N, K, act) in enumerate(SHAPES):
         if only is not None and idx not in only:
@@ -78,6 +97,8 @@ def main():
         for t in tiles:
             tf, ms = run(mode, M, N, K, act, t | args.flags, args.iters, dev, args.sink)
             cells.append(f"{tf:12.1f}" if tf is not None else f"{'n/a':>12s}")
+        if args.lib:
+            cells.append(f"{run_lib(M, N, K, args.iters, dev):12.1f}" if mode == "dense" else f"{'-':>12s}")
         print(f"{mode:8s} {M:7d} {N:5d} {K:5d} {act:3d} " + " ".join(cells), flush=True)
 
 

@@ -64,13 +64,20 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>((const bf16_t*)p.v + bat * p.bsv + h * 64), (short)0, (int)v_bytes, 0x00020000);
 
-  // Q^T fragments as the B operand: lane holds Q[q][16s + 8hh + j]
+  // Q^T fragments as the B operand: lane holds Q[q][16s + 8hh + j], prescaled by c = scale * log2(e)
+  // (rounded to bf16) so the S^T accumulators are scores in log2 units
+  const float c = p.scale * 1.4426950408889634f;
   bf16x8_t qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     uint4 t = make_uint4(0, 0, 0, 0);
     if (q < p.Sq) t = *reinterpret_cast<const uint4*>(qb + (size_t)q * p.ldq + 16 * s + 8 * hh);
-    qf[s] = *reinterpret_cast<bf16x8_t*>(&t);
+    const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = pack2(__uint_as_float(tw[j] << 16) * c, __uint_as_float(tw[j] & 0xffff0000u) * c);
+    qf[s] = *reinterpret_cast<bf16x8_t*>(w);
   }
 
   // DMA: wave w fills rows [8(w + NW u), +8) of each tile; lane -> (row, physical 16-B slot
@@ -96,11 +103,18 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
     }
   };
 
-  const float c = p.scale * 1.4426950408889634f;   // fold log2(e): p = exp2(s*c - m)
-  float m_run = -INFINITY, l_run = 0.0f;
-  f32x16_t o0, o1;
+  // Running max m (log2 units) per query, held NEGATED in all 16 entries of an accumulator-shaped
+  // vector: the first S^T MFMA of a tile accumulates onto it, so S^T comes out as s c - m, ready for
+  // v_exp with no per-score FMA. The max is deferred: m is raised (O and l rescaled, the tile
+  // exponentiated against the new m) only when some score of the tile exceeds it by more than
+  // FA_DEFER; otherwise p = exp2(s c - m) <= 2^FA_DEFER, well inside bf16 P / fp32 O and l range.
+  // The first tile always sets m. Per score the common path costs half a v_max3, one v_exp, one add
+  // and half a v_cvt_pk (the textbook loop adds an FMA per score and a rescale per max increase).
+  constexpr float FA_DEFER = 8.0f;
+  f32x16_t negm, o0, o1;
+  float l_run = 0.0f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { o0[r] = 0.0f; o1[r] = 0.0f; }
+  for (int r = 0; r < 16; ++r) { negm[r] = 0.0f; o0[r] = 0.0f; o1[r] = 0.0f; }
 
   // V transpose-read addressing: lane group g = lane / 16 covers d block (g & 1) * 16 (+32 for o1)
   // and keys 8 * rd + 4 * (g >> 1) + qq of the 16-key step (the k order of S^T's accumulator rows,
@@ -118,24 +132,22 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
     const char* kt = smem + buf * 2 * FA_TILE;
     const char* vt = kt + FA_TILE;
 
-    // ---- S^T = K Q^T for two 32-key subtiles ----
-    f32x16_t st[2];
+    // ---- S^T = K Q^T - m for two 32-key subtiles (all 8 K fragments read before the first MFMA) ----
+    bf16x8_t kf[2][4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[sub][r] = 0.0f;
       const int key = sub * 32 + r32;
       const char* kr = kt + key * 128;
       const int sk = fa_swk(key);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4));
-        st[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], st[sub], 0, 0, 0);
-      }
+      for (int s = 0; s < 4; ++s) kf[sub][s] = *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4));
     }
-    // ---- online softmax (lane = query column) ----
-    // running max in log2 units: m = c * max(s) (c > 0), p = exp2(c s - m) as one FMA + v_exp
-    float mx = -INFINITY;
+    f32x16_t st[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        st[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[sub][s], qf[s], s == 0 ? negm : st[sub], 0, 0, 0);
     if (kv0 + 64 > p.Skv) {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -143,21 +155,27 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
         for (int r = 0; r < 16; ++r)
           if (kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) st[sub][r] = -INFINITY;
     }
+    // ---- softmax numerators (lane = query column) ----
+    float mx = st[0][0];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[sub][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
-    const float m_new = fmaxf(m_run, mx);
-    // rescale only when some query's max grew (otherwise every alpha is exactly 1)
-    if (__any(m_new > m_run)) {
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      l_run *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      for (int r = (sub == 0 ? 1 : 0); r < 16; ++r) mx = fmaxf(mx, st[sub][r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
-    m_run = m_new;
-
+    if (kv0 == 0 || __any(!(mx <= FA_DEFER))) {    // rare: raise m (NaN-safe test)
+      const float dm = kv0 == 0 ? mx : fmaxf(mx, 0.0f);
+      if (kv0 > 0) {
+        const float alpha = __builtin_amdgcn_exp2f(-dm);
+        l_run *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { negm[r] -= dm; st[0][r] -= dm; st[1][r] -= dm; }
+    }
     bf16x8_t pf[2][2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
@@ -166,8 +184,8 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float p0 = __builtin_amdgcn_exp2f(fmaf(st[sub][8 * s2 + 2 * j], c, -m_new));
-          const float p1 = __builtin_amdgcn_exp2f(fmaf(st[sub][8 * s2 + 2 * j + 1], c, -m_new));
+          const float p0 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j]);
+          const float p1 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j + 1]);
           l_run += p0 + p1;
           w[j] = pack2(p0, p1);
         }

@@ -215,6 +215,27 @@ def test_flash_attn_peaked_scores(dev):
     assert rel(out, refo) < 2e-2
 
 
+@pytest.mark.parametrize("sign", [1.0, -1.0])
+def test_flash_attn_drifting_scores(dev, sign):
+    """Scores that grow (sign +1) or fall (-1) steadily across key blocks, far past the deferred-max
+    threshold: the kernel's running max must be raised tile after tile (or never)."""
+    nb, S, heads = 2, 1000, 1
+    C = heads * 64
+    g = torch.Generator().manual_seed(3)
+    d = torch.randn(64, generator=g)
+    d = d / d.norm()
+    q = d.expand(nb * S, 64) * 8.0 + 0.1 * torch.randn(nb * S, 64, generator=g)
+    ramp = torch.linspace(-1.0, 1.0, S).repeat(nb)[:, None] * sign
+    k = d.expand(nb * S, 64) * 12.0 * ramp + 0.5 * torch.randn(nb * S, 64, generator=g)
+    v = torch.randn(nb * S, 64, generator=g)
+    qkv = bf(torch.cat([q, k, v], 1))
+    out = ops.flash_attn(qkv.to(dev), nb, S, heads)
+    qf, kf, vf = qkv.float().view(nb, S, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    refo = F.scaled_dot_product_attention(qf, kf, vf).permute(0, 2, 1, 3).reshape(nb * S, C)
+    assert torch.isfinite(out.float()).all()
+    assert rel(out, refo) < 2e-2
+
+
 @pytest.mark.parametrize("B,F_,S,heads", [(2, 14, 37, 5), (1, 3, 16, 2), (4, 16, 9, 1)])
 def test_temporal_attn(dev, B, F_, S, heads):
     C = heads * 64

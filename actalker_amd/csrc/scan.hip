@@ -217,6 +217,13 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
 // in LDS (next tile prefetched into registers); outputs are gathered per tile in LDS and stored
 // with 16-byte coalesced writes.
 
+// softplus with the log taken by the raw v_log_f32 (log2): its argument 1 + exp(-|x|) lies in
+// [1, 2], so ocml's denormal range reduction around __logf is dead weight
+__device__ __forceinline__ float softplus_raw(float x) {
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+  return fmaxf(x, 0.0f) + __builtin_amdgcn_logf(1.0f + e) * 0.6931471805599453f;
+}
+
 __device__ __forceinline__ float pair_swap(float v) {
   // value of the partner lane (lane ^ 1): DPP quad_perm [1, 0, 3, 2]
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
@@ -247,11 +254,12 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
   const int dd = active ? d : 0;
   const bool rev = (k == 1) && p.flip1;
 
-  float w[R0P > 0 ? R0P : 1];
+  // dt_proj weights of this lane's half as pairs (packed FMAs: two products per v_pk_fma_f32)
+  f32x2_t w2[R0P > 0 ? R0P / 2 : 1];
 #pragma unroll
   for (int r = 0; r < R0P; ++r) {
     const int rr = half ? R0 + r : r;
-    w[r] = (r < R0 && rr < R) ? p.dt_w[((size_t)k * p.D + dd) * R + rr] : 0.0f;
+    w2[r / 2][r % 2] = (r < R0 && rr < R) ? p.dt_w[((size_t)k * p.D + dd) * R + rr] : 0.0f;
   }
   // zero the dt padding columns once (commit() never writes them; they meet zero weights)
   if (R > 0) {
@@ -262,11 +270,12 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
     }
   }
   const float bias = p.dt_b ? p.dt_b[k * p.D + dd] : 0.0f;
-  float a2[8], h[8];
+  // this lane's 8 states as 4 pairs: A * log2(e) and h
+  f32x2_t a2[4], h[4];
 #pragma unroll
   for (int n = 0; n < 8; ++n) {
-    a2[n] = -__expf(p.A_log[((size_t)k * p.D + dd) * 16 + 8 * half + n]) * 1.4426950408889634f;
-    h[n] = 0.0f;
+    a2[n / 2][n % 2] = -__expf(p.A_log[((size_t)k * p.D + dd) * 16 + 8 * half + n]) * 1.4426950408889634f;
+    h[n / 2][n % 2] = 0.0f;
   }
   const float dsk = p.Dskip ? p.Dskip[k * p.D + dd] : 0.0f;
 
@@ -350,31 +359,34 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
         dt = dls[tt * SP_CH + cl] + bias;
       } else {
         const float4* xr4 = reinterpret_cast<const float4*>(xr + half * R0P);
-        float part = 0.0f;
+        f32x2_t part = {0.0f, 0.0f};
 #pragma unroll
         for (int r4 = 0; r4 < R0P / 4; ++r4) {
           const float4 v = xr4[r4];
-          part = fmaf(w[4 * r4], v.x, part);
-          part = fmaf(w[4 * r4 + 1], v.y, part);
-          part = fmaf(w[4 * r4 + 2], v.z, part);
-          part = fmaf(w[4 * r4 + 3], v.w, part);
+          part = __builtin_elementwise_fma(w2[2 * r4], (f32x2_t){v.x, v.y}, part);
+          part = __builtin_elementwise_fma(w2[2 * r4 + 1], (f32x2_t){v.z, v.w}, part);
         }
-        dt = part + pair_swap(part) + bias;
+        const float ph = part.x + part.y;
+        dt = ph + pair_swap(ph) + bias;
       }
-      if (SOFTPLUS) dt = softplus_fast(dt);
+      if (SOFTPLUS) dt = softplus_raw(dt);
       const float uu = bf2f(us[tt * SP_CH + cl]);
       const float du = dt * uu;
       const float4* bv = reinterpret_cast<const float4*>(xr + 2 * R0P + 8 * half);
       const float4* cv = reinterpret_cast<const float4*>(xr + 2 * R0P + 16 + 8 * half);
       const float4 b0 = bv[0], b1 = bv[1], c0 = cv[0], c1 = cv[1];
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      const float cc8[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      float y = 0.0f;
+      const f32x2_t bb[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
+      const f32x2_t cc[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
+      const f32x2_t dt2 = {dt, dt}, du2 = {du, du};
+      f32x2_t y2 = {0.0f, 0.0f};
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        h[n] = fmaf(fast_exp2(dt * a2[n]), h[n], du * bb[n]);
-        y = fmaf(h[n], cc8[n], y);
+      for (int n = 0; n < 4; ++n) {
+        const f32x2_t x = dt2 * a2[n];
+        const f32x2_t e = {fast_exp2(x.x), fast_exp2(x.y)};
+        h[n] = __builtin_elementwise_fma(e, h[n], du2 * bb[n]);
+        y2 = __builtin_elementwise_fma(h[n], cc[n], y2);
       }
+      float y = y2.x + y2.y;
       y += pair_swap(y);
       if (half == 0) ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uu, y));
     };

@@ -119,6 +119,18 @@ class ScanDesc(ctypes.Structure):
     ]
 
 
+class ConvDirectDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_int),
+        ("w", c_vp), ("bias", c_vp),
+        ("y", c_vp), ("ldy", c_int),
+        ("mode", c_int),
+        ("B", c_int), ("H", c_int), ("W", c_int), ("Ho", c_int), ("Wo", c_int), ("stride", c_int),
+        ("F", c_int), ("S", c_int),
+        ("Cin", c_int), ("Cout", c_int), ("act", c_int), ("out_f32", c_int),
+    ]
+
+
 # Every symbol include/actalker_hip.h declares, with its ctypes signature.
 _P = ctypes.POINTER
 SIGNATURES = {
@@ -133,6 +145,8 @@ SIGNATURES = {
     "acth_mamba_combine_ln": ([_P(MambaCombineDesc), c_vp], c_int),
     "acth_selective_scan": ([_P(ScanDesc), c_vp], c_int),
     "acth_selective_scan_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
+    "acth_conv_direct": ([_P(ConvDirectDesc), c_vp], c_int),
+    "acth_softmax_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_float, c_vp], c_int),
     "acth_timestep_embedding": ([c_vp, c_int, c_int, c_int, c_float, c_float, c_float, c_vp, c_vp], c_int),
     "acth_nchw_to_tokens": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
     "acth_tokens_to_nchw": ([c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),

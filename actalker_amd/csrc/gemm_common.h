@@ -163,6 +163,9 @@ __device__ __forceinline__ void epilogue8_tail(const ActhGemmDesc& p, int row, i
   } else if (p.act == 3) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = gelu_erf(v[k]);
+  } else if (p.act == 4) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.0f);
   }
   if (p.MIX) {
     float t[8];
@@ -215,6 +218,9 @@ __device__ __forceinline__ void epilogue8(const ActhGemmDesc& p, int row, int oc
   } else if (p.act == 3) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+  } else if (p.act == 4) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
   }
   if (p.MIX) {
     const bf16_t* mp = (const bf16_t*)p.MIX + (size_t)row * p.ldmix + ocol;

@@ -482,3 +482,45 @@ extern "C" int acth_mamba_combine_ln(const ActhMambaCombineDesc* d, hipStream_t 
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// Row softmax y = softmax(scale * x) of fp32 score rows into bf16 probabilities: the middle of the
+// materialised single-head (head_dim 512) attention of the VAE mid blocks (diffusers Attention with
+// upcast_softmax=True, AttnProcessor2_0), where S x S scores per frame fit HBM easily and the two
+// contractions run on the MFMA GEMM. One block per row; fp32 max / sum; three passes over the row
+// (max, sum of exponentials, write), the row (<= 36 KB at S = 9216) staying in L2 between passes.
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = is_max ? fmaxf(r, sh[i]) : r + sh[i];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* x, int ldx, bf16_t* y, int ldy, int cols,
+                                                           float scale_log2) {
+  __shared__ float sh[4];
+  const float* xr = x + (long long)blockIdx.x * ldx;
+  bf16_t* yr = y + (long long)blockIdx.x * ldy;
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, xr[c]);
+  m = block_reduce(m, sh, true) * scale_log2;
+  float s = 0.0f;
+  for (int c = threadIdx.x; c < cols; c += 256) s += __builtin_amdgcn_exp2f(fmaf(xr[c], scale_log2, -m));
+  s = block_reduce(s, sh, false);
+  const float inv = 1.0f / s;
+  for (int c = threadIdx.x; c < cols; c += 256) yr[c] = f2bf(__builtin_amdgcn_exp2f(fmaf(xr[c], scale_log2, -m)) * inv);
+}
+
+extern "C" int acth_softmax_rows(const float* x, int ldx, void* y, int ldy, int rows, int cols, float scale,
+                                 hipStream_t stream) {
+  if (!x || !y || rows < 0 || cols <= 0 || ldx < cols || ldy < cols || !(scale > 0.0f)) return ACTH_EINVAL;
+  if (rows == 0) return ACTH_OK;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)rows), dim3(256), 0, stream, x, ldx, (bf16_t*)y, ldy, cols,
+                     scale * 1.4426950408889634f);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}

@@ -14,7 +14,7 @@ import torch
 
 from . import _lib
 
-ACT_NONE, ACT_SILU, ACT_GEGLU, ACT_GELU = 0, 1, 2, 3
+ACT_NONE, ACT_SILU, ACT_GEGLU, ACT_GELU, ACT_RELU = 0, 1, 2, 3, 4
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -448,4 +448,65 @@ def cfg_euler_accum(noise, unit_off, lat, frame_idx, g1, g2, g3, sigma, sigma_ne
 def div_counter(acc, cnt, out, T, S):
     lib = _lib.load()
     _lib.check(lib.acth_div_counter(_p(acc), _p(cnt), _p(out), T, S, _stream()), "acth_div_counter")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+def pack_conv_direct(w: torch.Tensor) -> torch.Tensor:
+    """Conv weight (Cout, Cin, 3, 3) or (Cout, Cin, 3, 1, 1) -> fp32 (taps*Cin, Cout), k = tap*Cin + c."""
+    w = w.detach().float()
+    if w.dim() == 5:
+        w = w[:, :, :, 0, 0]                                  # (Cout, Cin, 3)
+        return w.permute(2, 1, 0).reshape(-1, w.shape[0]).contiguous()
+    return w.permute(2, 3, 1, 0).reshape(-1, w.shape[0]).contiguous()
+
+
+def conv_direct(x: torch.Tensor, wp: torch.Tensor, bias: Optional[torch.Tensor], *, B: int, H: int = 0, W: int = 0,
+                stride: int = 1, temporal: Optional[dict] = None, act: int = ACT_NONE, out_f32: bool = False,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Direct 3x3 (pad 1, stride 1/2) or (3,1,1) temporal conv on NHWC rows for narrow channels.
+    ``wp`` from :func:`pack_conv_direct`; ``temporal=dict(F, S)`` selects the frame-axis form."""
+    lib = _lib.load()
+    _need(x, torch.bfloat16, "conv_direct x")
+    _need(wp, torch.float32, "conv_direct w")
+    Cin = x.shape[1] if x.dim() == 2 else None
+    taps = 3 if temporal is not None else 9
+    if Cin is None or wp.shape[0] != taps * Cin:
+        raise _lib.ActhError(f"conv_direct: weight rows {wp.shape[0]} != {taps}*Cin ({Cin})")
+    Cout = wp.shape[1]
+    d = _lib.ConvDirectDesc()
+    if temporal is None:
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        if x.shape[0] != B * H * W:
+            raise _lib.ActhError(f"conv_direct: x has {x.shape[0]} rows, expected {B * H * W}")
+        d.mode, d.H, d.W, d.Ho, d.Wo, d.stride = 0, H, W, Ho, Wo, stride
+        M = B * Ho * Wo
+    else:
+        Fr, S = temporal["F"], temporal["S"]
+        if x.shape[0] != B * Fr * S:
+            raise _lib.ActhError(f"conv_direct: x has {x.shape[0]} rows, expected {B * Fr * S}")
+        d.mode, d.F, d.S = 1, Fr, S
+        M = B * Fr * S
+    if out is None:
+        out = torch.empty((M, Cout), device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    d.x, d.ldx = x.data_ptr(), _rows(x, "conv_direct x")
+    d.w = wp.data_ptr()
+    if bias is not None:
+        _need(bias, torch.float32, "conv_direct bias")
+        d.bias = bias.data_ptr()
+    d.y, d.ldy = out.data_ptr(), _rows(out, "conv_direct out")
+    d.B, d.Cin, d.Cout, d.act, d.out_f32 = B, Cin, Cout, act, int(out_f32)
+    _lib.check(lib.acth_conv_direct(ctypes.byref(d), _stream()), "acth_conv_direct")
+    return out
+
+
+def softmax_rows(x: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 softmax(scale * x) over the last dim of an fp32 (rows, cols) matrix."""
+    lib = _lib.load()
+    _need(x, torch.float32, "softmax x")
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty((rows, cols), device=x.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_softmax_rows(_p(x), _rows(x, "softmax x"), _p(out), _rows(out, "softmax out"), rows, cols,
+                                     float(scale), _stream()), "acth_softmax_rows")
     return out

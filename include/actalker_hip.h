@@ -47,7 +47,7 @@ typedef struct ActhGemmDesc {
   const void* R; int ldr; const int* rmap; int r_div, r_mod;
   const void* MIX; int ldmix; float mix_alpha;
   float alpha;
-  int act;                   /* 0 none, 1 silu, 2 geglu (interleaved 16-col granules), 3 gelu */
+  int act;                   /* 0 none, 1 silu, 2 geglu (interleaved 16-col granules), 3 gelu, 4 relu */
   int out_f32;
   void* C; int ldc;
   int orow_div, orow_stride, orow_off;
@@ -145,6 +145,25 @@ typedef struct ActhScanDesc {
 } ActhScanDesc;
 int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream);
 size_t acth_selective_scan_workspace_size(int nb, int G, int D, int nchunks);
+
+/* ---- direct 3x3 (pad 1, stride 1/2) / temporal (3,1,1) convolution for narrow channel counts
+ * (PoseGuider InflatedConv3d, pose_guider.py:17-73; VAE TemporalDecoder conv_out / time_conv_out).
+ * x: NHWC bf16 rows; w: fp32 (taps*Cin, Cout), k = tap*Cin + c (tap = ky*3 + kx, or the frame tap);
+ * y: rows (B*Ho*Wo | B*F*S, ldy), bf16 or fp32; act 0 none / 1 silu */
+typedef struct ActhConvDirectDesc {
+  const void* x; int ldx;
+  const float* w; const float* bias;
+  void* y; int ldy;
+  int mode;                  /* 0 spatial 3x3, 1 temporal 3-tap over F frames (rows (b*F + f)*S + s) */
+  int B, H, W, Ho, Wo, stride;
+  int F, S;
+  int Cin, Cout, act, out_f32;
+} ActhConvDirectDesc;
+int acth_conv_direct(const ActhConvDirectDesc* d, hipStream_t stream);
+
+/* ---- y(bf16) = softmax(scale * x(fp32)) per row (VAE mid-block single-head attention) */
+int acth_softmax_rows(const float* x, int ldx, void* y, int ldy, int rows, int cols, float scale,
+                      hipStream_t stream);
 
 /* ---- small kernels */
 int acth_timestep_embedding(const float* t, int n, int dim, int flip_sin_to_cos, float downscale_freq_shift,

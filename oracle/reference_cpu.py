@@ -408,6 +408,50 @@ def unet_forward(sd: SD, sample, timestep, encoder_hidden_states, added_time_ids
     return x.reshape(B, Fn, *x.shape[1:])
 
 
+# ============================================================================ conditioning adapters
+def _k(p: str, name: str) -> str:
+    return name if not p else p + "." + name
+
+
+def audio_proj_model(sd: SD, p: str, audio_embeds, context_tokens=32):
+    """AudioProjModel.forward (src/models/audio_adapter/audio_proj.py:103-130)."""
+    bz, f = audio_embeds.shape[:2]
+    x = audio_embeds.reshape(bz * f, -1)
+    x = F.relu(linear(sd, _k(p, "proj1"), x))
+    x = F.relu(linear(sd, _k(p, "proj2"), x))
+    x = linear(sd, _k(p, "proj3"), x).reshape(bz * f, context_tokens, -1)
+    x = layer_norm(sd, _k(p, "norm"), x)
+    return x.reshape(bz, f, context_tokens, -1)
+
+
+def vasa_proj_model(sd: SD, p: str, x):
+    """VasaProjModel.forward (audio_proj.py:147-150)."""
+    return layer_norm(sd, _k(p, "norm"), linear(sd, _k(p, "proj1"), x))
+
+
+def id_proj_model(sd: SD, p: str, x):
+    """IDProjModel.forward (audio_proj.py:162-170); ExpProjModel (:181-189) is the same MLP."""
+    x = F.relu(linear(sd, _k(p, "proj1"), x))
+    x = F.relu(linear(sd, _k(p, "proj2"), x))
+    return linear(sd, _k(p, "proj3"), x)
+
+
+def pose_guider(sd: SD, p: str, cond, n_blocks: int = 6):
+    """PoseGuider.forward (pose_guider.py:63-73): InflatedConv3d = Conv2d per frame (:17-25)."""
+    b, c, f, h, w = cond.shape
+
+    def conv(name, x, stride=1):
+        y = F.conv2d(x, sd[_k(p, name + ".weight")], sd[_k(p, name + ".bias")], stride=stride, padding=1)
+        return y
+
+    x = cond.permute(0, 2, 1, 3, 4).reshape(b * f, c, h, w)
+    x = F.silu(conv("conv_in", x))
+    for i in range(n_blocks):
+        x = F.silu(conv(f"blocks.{i}", x, stride=1 if i % 2 == 0 else 2))
+    x = conv("conv_out", x)
+    return x.reshape(b, f, *x.shape[1:]).permute(0, 2, 1, 3, 4)
+
+
 # ============================================================================ scheduler + loop
 def euler_karras_tables(num_inference_steps: int = 25, sigma_min: float = 0.002, sigma_max: float = 700.0,
                         rho: float = 7.0):

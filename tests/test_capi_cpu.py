@@ -34,7 +34,8 @@ def test_struct_layouts_match_header():
     for cname, py in (("ActhGemmDesc", _lib.GemmDesc), ("ActhAttnDesc", _lib.AttnDesc),
                       ("ActhTemporalAttnDesc", _lib.TemporalAttnDesc), ("ActhIpAttnDesc", _lib.IpAttnDesc),
                       ("ActhLayerNormDesc", _lib.LayerNormDesc), ("ActhGroupNormDesc", _lib.GroupNormDesc),
-                      ("ActhMambaCombineDesc", _lib.MambaCombineDesc), ("ActhScanDesc", _lib.ScanDesc)):
+                      ("ActhMambaCombineDesc", _lib.MambaCombineDesc), ("ActhScanDesc", _lib.ScanDesc),
+                      ("ActhConvDirectDesc", _lib.ConvDirectDesc)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, flags=re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = re.findall(r"(\w+)\s*(?:,|;)", body)
@@ -55,6 +56,13 @@ def test_invalid_arguments_rejected_without_launch():
     a = _lib.TemporalAttnDesc()
     a.qkv, a.o, a.F, a.B, a.S, a.H = 16, 16, 17, 1, 1, 1                   # F > 16
     assert lib.acth_temporal_attn(ctypes.byref(a), None) == -1
+    c = _lib.ConvDirectDesc()
+    c.x, c.w, c.y, c.Cin, c.Cout, c.ldx, c.ldy, c.B, c.H, c.W, c.Ho, c.Wo = 16, 16, 16, 3, 16, 3, 16, 1, 8, 8, 8, 8
+    c.stride = 3                                                            # stride must be 1 or 2
+    assert lib.acth_conv_direct(ctypes.byref(c), None) == -1
+    c.stride, c.Ho = 2, 8                                                   # Ho != (H-1)//2 + 1
+    assert lib.acth_conv_direct(ctypes.byref(c), None) == -1
+    assert lib.acth_softmax_rows(16, 4, 16, 8, 2, 8, 1.0, None) == -1        # ldx < cols
 
 
 def test_no_cpu_fallback():

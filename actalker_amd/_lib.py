@@ -126,6 +126,7 @@ class ConvDirectDesc(ctypes.Structure):
         ("y", c_vp), ("ldy", c_int),
         ("mode", c_int),
         ("B", c_int), ("H", c_int), ("W", c_int), ("Ho", c_int), ("Wo", c_int), ("stride", c_int),
+        ("pad0", c_int),
         ("F", c_int), ("S", c_int),
         ("Cin", c_int), ("Cout", c_int), ("act", c_int), ("out_f32", c_int),
     ]

@@ -21,7 +21,8 @@ __device__ __forceinline__ long long in_row(const ActhConvDirectDesc& p, long lo
     const int r = (int)(m - b * HWo);
     const int yo = r / p.Wo, xo = r - (r / p.Wo) * p.Wo;
     const int ky = tap / 3, kx = tap - ky * 3;
-    const int yi = yo * p.stride - 1 + ky, xi = xo * p.stride - 1 + kx;
+    const int lo = p.pad0 ? 0 : 1;          // pad0: F.pad(0, 1, 0, 1) + padding 0 (Downsample2D padding=0)
+    const int yi = yo * p.stride - lo + ky, xi = xo * p.stride - lo + kx;
     ok = (yi >= 0) && (yi < p.H) && (xi >= 0) && (xi < p.W);
     return (b * p.H + yi) * p.W + xi;
   }
@@ -129,7 +130,10 @@ extern "C" int acth_conv_direct(const ActhConvDirectDesc* d, hipStream_t stream)
   long long Mout;
   if (d->mode == 0) {
     if (d->B <= 0 || d->H <= 0 || d->W <= 0 || (d->stride != 1 && d->stride != 2)) return ACTH_EINVAL;
-    if (d->Ho != (d->H - 1) / d->stride + 1 || d->Wo != (d->W - 1) / d->stride + 1) return ACTH_EINVAL;
+    const int padsum = d->pad0 ? 1 : 2;
+    if (d->H + padsum < 3 || d->W + padsum < 3) return ACTH_EINVAL;
+    if (d->Ho != (d->H + padsum - 3) / d->stride + 1 || d->Wo != (d->W + padsum - 3) / d->stride + 1)
+      return ACTH_EINVAL;
     Mout = (long long)d->B * d->Ho * d->Wo;
   } else if (d->mode == 1) {
     if (d->B <= 0 || d->F <= 0 || d->S <= 0) return ACTH_EINVAL;

@@ -201,7 +201,8 @@ class ResnetBlock2D(nn.Module):
         self.in_channels, self.out_channels = in_channels, out_channels
         self.norm1 = GroupNorm(32, in_channels, eps=eps, affine=True)
         self.conv1 = Conv2d(in_channels, out_channels, 3, 1, 1)
-        self.time_emb_proj = Linear(temb_channels, out_channels)
+        # temb_channels=None: no time embedding (the VAE's blocks, diffusers resnet.py)
+        self.time_emb_proj = Linear(temb_channels, out_channels) if temb_channels is not None else None
         self.norm2 = GroupNorm(32, out_channels, eps=eps, affine=True)
         self.dropout = nn.Dropout(0.0)
         self.conv2 = Conv2d(out_channels, out_channels, 3, 1, 1)
@@ -232,7 +233,7 @@ class TemporalResnetBlock(nn.Module):
         self.in_channels, self.out_channels = in_channels, out_channels
         self.norm1 = GroupNorm(32, in_channels, eps=eps, affine=True)
         self.conv1 = Conv3d(in_channels, out_channels, kernel_size=(3, 1, 1), stride=1, padding=(1, 0, 0))
-        self.time_emb_proj = Linear(temb_channels, out_channels)
+        self.time_emb_proj = Linear(temb_channels, out_channels) if temb_channels is not None else None
         self.norm2 = GroupNorm(32, out_channels, eps=eps, affine=True)
         self.dropout = nn.Dropout(0.0)
         self.conv2 = Conv3d(out_channels, out_channels, kernel_size=(3, 1, 1), stride=1, padding=(1, 0, 0))

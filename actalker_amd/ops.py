@@ -462,10 +462,11 @@ def pack_conv_direct(w: torch.Tensor) -> torch.Tensor:
 
 
 def conv_direct(x: torch.Tensor, wp: torch.Tensor, bias: Optional[torch.Tensor], *, B: int, H: int = 0, W: int = 0,
-                stride: int = 1, temporal: Optional[dict] = None, act: int = ACT_NONE, out_f32: bool = False,
+                stride: int = 1, pad0: bool = False, temporal: Optional[dict] = None, act: int = ACT_NONE, out_f32: bool = False,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Direct 3x3 (pad 1, stride 1/2) or (3,1,1) temporal conv on NHWC rows for narrow channels.
-    ``wp`` from :func:`pack_conv_direct`; ``temporal=dict(F, S)`` selects the frame-axis form."""
+    ``wp`` from :func:`pack_conv_direct`; ``temporal=dict(F, S)`` selects the frame-axis form; ``pad0``
+    pads only bottom/right (diffusers Downsample2D with padding=0: F.pad(x, (0, 1, 0, 1)), conv pad 0)."""
     lib = _lib.load()
     _need(x, torch.bfloat16, "conv_direct x")
     _need(wp, torch.float32, "conv_direct w")
@@ -476,10 +477,11 @@ def conv_direct(x: torch.Tensor, wp: torch.Tensor, bias: Optional[torch.Tensor],
     Cout = wp.shape[1]
     d = _lib.ConvDirectDesc()
     if temporal is None:
-        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        ps = 1 if pad0 else 2
+        Ho, Wo = (H + ps - 3) // stride + 1, (W + ps - 3) // stride + 1
         if x.shape[0] != B * H * W:
             raise _lib.ActhError(f"conv_direct: x has {x.shape[0]} rows, expected {B * H * W}")
-        d.mode, d.H, d.W, d.Ho, d.Wo, d.stride = 0, H, W, Ho, Wo, stride
+        d.mode, d.H, d.W, d.Ho, d.Wo, d.stride, d.pad0 = 0, H, W, Ho, Wo, stride, int(pad0)
         M = B * Ho * Wo
     else:
         Fr, S = temporal["F"], temporal["S"]

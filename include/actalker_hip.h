@@ -147,7 +147,8 @@ int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream);
 size_t acth_selective_scan_workspace_size(int nb, int G, int D, int nchunks);
 
 /* ---- direct 3x3 (pad 1, stride 1/2) / temporal (3,1,1) convolution for narrow channel counts
- * (PoseGuider InflatedConv3d, pose_guider.py:17-73; VAE TemporalDecoder conv_out / time_conv_out).
+ * (PoseGuider InflatedConv3d, pose_guider.py:17-73; VAE Encoder conv_in / downsamplers, TemporalDecoder
+ * conv_in / conv_out / time_conv_out).
  * x: NHWC bf16 rows; w: fp32 (taps*Cin, Cout), k = tap*Cin + c (tap = ky*3 + kx, or the frame tap);
  * y: rows (B*Ho*Wo | B*F*S, ldy), bf16 or fp32; act 0 none / 1 silu */
 typedef struct ActhConvDirectDesc {
@@ -156,6 +157,7 @@ typedef struct ActhConvDirectDesc {
   void* y; int ldy;
   int mode;                  /* 0 spatial 3x3, 1 temporal 3-tap over F frames (rows (b*F + f)*S + s) */
   int B, H, W, Ho, Wo, stride;
+  int pad0;                  /* mode 0: 0 = padding 1 all sides; 1 = bottom/right only (diffusers Downsample2D padding=0) */
   int F, S;
   int Cin, Cout, act, out_f32;
 } ActhConvDirectDesc;

@@ -452,6 +452,91 @@ def pose_guider(sd: SD, p: str, cond, n_blocks: int = 6):
     return x.reshape(b, f, *x.shape[1:]).permute(0, 2, 1, 3, 4)
 
 
+# ============================================================================ VAE
+# diffusers 0.29.2 AutoencoderKLTemporalDecoder (Inference.py:41-44; used at pipeline:235-290, :520-536,
+# :766). diffusers is absent here: restated from the pinned version's published source.
+def vae_resnet2d(sd: SD, p: str, x, eps=1e-6):
+    """ResnetBlock2D with temb_channels=None (resnet.py)."""
+    h = F.silu(group_norm(sd, p + ".norm1", x, eps))
+    h = F.conv2d(h, sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], padding=1)
+    h = F.silu(group_norm(sd, p + ".norm2", h, eps))
+    h = F.conv2d(h, sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], padding=1)
+    if p + ".conv_shortcut.weight" in sd:
+        x = F.conv2d(x, sd[p + ".conv_shortcut.weight"], sd[p + ".conv_shortcut.bias"])
+    return x + h
+
+
+def vae_temporal_resnet(sd: SD, p: str, x, eps=1e-5):
+    """TemporalResnetBlock with temb None on (B, C, F, H, W)."""
+    h = F.silu(group_norm(sd, p + ".norm1", x, eps))
+    h = F.conv3d(h, sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], padding=(1, 0, 0))
+    h = F.silu(group_norm(sd, p + ".norm2", h, eps))
+    h = F.conv3d(h, sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], padding=(1, 0, 0))
+    return x + h
+
+
+def vae_st_resblock(sd: SD, p: str, x, num_frames):
+    """SpatioTemporalResBlock(temb None, eps 1e-6, temporal_eps 1e-5, merge 'learned',
+    switch_spatial_to_temporal_mix=True): AlphaBlender alpha = 1 - sigmoid(mix_factor)."""
+    h = vae_resnet2d(sd, p + ".spatial_res_block", x, 1e-6)
+    bf, c, hh, ww = h.shape
+    b = bf // num_frames
+    h5 = h.reshape(b, num_frames, c, hh, ww).permute(0, 2, 1, 3, 4)
+    t = vae_temporal_resnet(sd, p + ".temporal_res_block", h5, 1e-5)
+    a = 1.0 - torch.sigmoid(sd[p + ".time_mixer.mix_factor"])
+    out = a * h5 + (1.0 - a) * t
+    return out.permute(0, 2, 1, 3, 4).reshape(bf, c, hh, ww)
+
+
+def vae_attention(sd: SD, p: str, x, eps=1e-6):
+    """Attention(heads=1, dim_head=C, norm_num_groups=32, residual_connection, bias) under AttnProcessor2_0
+    on a 4-D input (attention_processor.py:1528-1605 semantics)."""
+    B, C, H, W = x.shape
+    h = x.view(B, C, H * W)
+    h = group_norm(sd, p + ".group_norm", h, eps).transpose(1, 2)
+    q, k, v = (linear(sd, p + n, h) for n in (".to_q", ".to_k", ".to_v"))
+    o = F.scaled_dot_product_attention(q[:, None], k[:, None], v[:, None])[:, 0]
+    o = linear(sd, p + ".to_out.0", o).transpose(1, 2).reshape(B, C, H, W)
+    return o + x
+
+
+def vae_decode(sd: SD, z, num_frames, p: str = "decoder", n_up: int = 4, layers_per_block: int = 2):
+    """AutoencoderKLTemporalDecoder.decode -> TemporalDecoder.forward (image_only_indicator zeros)."""
+    x = F.conv2d(z, sd[p + ".conv_in.weight"], sd[p + ".conv_in.bias"], padding=1)
+    x = vae_st_resblock(sd, p + ".mid_block.resnets.0", x, num_frames)
+    for i in range(1, layers_per_block):
+        x = vae_attention(sd, p + f".mid_block.attentions.{i - 1}", x)
+        x = vae_st_resblock(sd, p + f".mid_block.resnets.{i}", x, num_frames)
+    for u in range(n_up):
+        for r in range(layers_per_block + 1):
+            x = vae_st_resblock(sd, p + f".up_blocks.{u}.resnets.{r}", x, num_frames)
+        if p + f".up_blocks.{u}.upsamplers.0.conv.weight" in sd:
+            x = upsample_2d(sd, p + f".up_blocks.{u}.upsamplers.0", x)
+    x = F.silu(group_norm(sd, p + ".conv_norm_out", x, 1e-6))
+    x = F.conv2d(x, sd[p + ".conv_out.weight"], sd[p + ".conv_out.bias"], padding=1)
+    bf, c, hh, ww = x.shape
+    x = x.reshape(bf // num_frames, num_frames, c, hh, ww).permute(0, 2, 1, 3, 4)
+    x = F.conv3d(x, sd[p + ".time_conv_out.weight"], sd[p + ".time_conv_out.bias"], padding=(1, 0, 0))
+    return x.permute(0, 2, 1, 3, 4).reshape(bf, c, hh, ww)
+
+
+def vae_encode_moments(sd: SD, x, p: str = "encoder", n_down: int = 4, layers_per_block: int = 2):
+    """Encoder.forward + quant_conv -> moments (B, 8, H/8, W/8); latent_dist.mean = moments[:, :4]."""
+    x = F.conv2d(x, sd[p + ".conv_in.weight"], sd[p + ".conv_in.bias"], padding=1)
+    for d in range(n_down):
+        for r in range(layers_per_block):
+            x = vae_resnet2d(sd, p + f".down_blocks.{d}.resnets.{r}", x, 1e-6)
+        q = p + f".down_blocks.{d}.downsamplers.0.conv"
+        if q + ".weight" in sd:   # Downsample2D(padding=0): pad right/bottom by one, conv stride 2
+            x = F.conv2d(F.pad(x, (0, 1, 0, 1)), sd[q + ".weight"], sd[q + ".bias"], stride=2)
+    x = vae_resnet2d(sd, p + ".mid_block.resnets.0", x, 1e-6)
+    x = vae_attention(sd, p + ".mid_block.attentions.0", x)
+    x = vae_resnet2d(sd, p + ".mid_block.resnets.1", x, 1e-6)
+    x = F.silu(group_norm(sd, p + ".conv_norm_out", x, 1e-6))
+    x = F.conv2d(x, sd[p + ".conv_out.weight"], sd[p + ".conv_out.bias"], padding=1)
+    return F.conv2d(x, sd["quant_conv.weight"], sd["quant_conv.bias"])
+
+
 # ============================================================================ scheduler + loop
 def euler_karras_tables(num_inference_steps: int = 25, sigma_min: float = 0.002, sigma_max: float = 700.0,
                         rho: float = 7.0):

@@ -43,13 +43,14 @@ def karras_sigmas(num_inference_steps: int = 25, sigma_min: float = 0.002, sigma
 
 
 # ------------------------------------------------------------------------------------------ planning
+def window_frames_raw(T: int, fpb: int, overlap: int, shift: int) -> List[List[int]]:
+    """Unwrapped frame indices of every window at a step (pipeline:684-694): start - shift + j."""
+    return [[index_start - shift + j for j in range(fpb)] for index_start in range(0, T, fpb - overlap)]
+
+
 def window_frames(T: int, fpb: int, overlap: int, shift: int) -> List[List[int]]:
-    """Frame indices of every window at a step (pipeline:684-694): start - shift, wrapped mod T."""
-    out = []
-    for index_start in range(0, T, fpb - overlap):
-        s = index_start - shift
-        out.append([(s + j) % T for j in range(fpb)])
-    return out
+    """Frame indices of every window at a step, wrapped mod T (indice_slice, pipeline:687-693)."""
+    return [[r % T for r in win] for win in window_frames_raw(T, fpb, overlap, shift)]
 
 
 def assign_units(n_windows: int, world: int, rank: int, n_branch: int = 4) -> Tuple[List[Tuple[int, int]], int]:
@@ -109,8 +110,15 @@ class HipBackend:
         self.aud = (audio_prompts.to(dev, torch.float32) * self.gate[0]).to(torch.bfloat16)        # (nb, T, 32, 1024)
         self.n_audio = self.aud.shape[2]
         self.vas = (vasa_prompts.to(dev, torch.float32) * self.gate[1]).to(torch.bfloat16).reshape(nb, T, -1)
-        self.pose = ops.nchw_to_tokens(pose_fea.to(dev))                                            # (T*S, 320)
+        self.pose = ops.nchw_to_tokens(pose_fea.to(dev))                                            # (P*S, 320)
+        # pose features may hold P != T frames (the pipeline's pose list has N frames): the reference
+        # indexes them with the raw window index mod P (indice_slice, pipeline:687-693), not mod T
+        self.pose_P = pose_fea.shape[1]
+        self._raw = None
         self.added = added_time_ids.to(dev, torch.float32)                                          # (nb, 3)
+
+    def begin_step(self, raw_frames: List[List[int]]):
+        self._raw = raw_frames
 
     def new_state(self, latents_all: torch.Tensor) -> torch.Tensor:
         return self.ops.nchw_to_tokens(latents_all.to(self.dev).float(), out_dtype=torch.float32)  # (T*S, 4)
@@ -131,8 +139,12 @@ class HipBackend:
         ehs = (self.ide[bl, fl], [self.aud[bl, fl], self.vas[bl, fl]])
         cak = {"ip_adapter_masks": self.masks, "acth_gate": self.gate}
         tt = torch.full((1,), t, device=self.dev, dtype=torch.float32)
+        prmap = fidx_d
+        if self.pose_P != self.T:
+            prmap = torch.tensor([r % self.pose_P for (w, _c) in units for r in self._raw[w]],
+                                 dtype=torch.int32).to(self.dev, non_blocking=True)
         noise = self.unet.forward_tokens(x, U, F, self.H, self.W, tt, ehs, self.added[br_d], self.pose, cak,
-                                         spatial_condition_rmap=fidx_d, out_f32=True)
+                                         spatial_condition_rmap=prmap, out_f32=True)
         out[row0:row0 + U * F * S].copy_(noise)
 
     def step_windows(self, lat, gathered, unit_rows: List[List[int]], frames, guidance, sigma, sigma_next):
@@ -161,6 +173,8 @@ class LoopConfig:
     shift_offset: int = 7
     num_inference_steps: int = 25
     guidance: Tuple[float, float, float] = (2.0, 7.5, 3.0)
+    # per-step (g1, g2, g3) = linspace(min, max, steps)[i] (pipeline:640-657); None: constant ``guidance``
+    guidance_schedule: Optional[List[Tuple[float, float, float]]] = None
     sigma_min: float = 0.002
     sigma_max: float = 700.0
     units_per_call: int = 4
@@ -199,6 +213,8 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
         streams = [torch.cuda.Stream(device=lat.device) for _ in range(min(cfg.concurrent_calls, len(calls)))]
     for i in range(n_steps):
         frames = window_frames(T, F, cfg.overlap, shift)
+        if hasattr(backend, "begin_step"):
+            backend.begin_step(window_frames_raw(T, F, cfg.overlap, shift))
         if streams:
             main = torch.cuda.current_stream(lat.device)
             for s in streams:
@@ -217,7 +233,8 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
             import torch.distributed as dist
             dist.all_gather_into_tensor(gathered, local, group=group)
         unit_rows = [[unit_row[w * 4 + c] for c in range(4)] for w in range(n_windows)]
-        lat = backend.step_windows(lat, gathered, unit_rows, frames, cfg.guidance, sigmas[i], sigmas[i + 1])
+        g = cfg.guidance if cfg.guidance_schedule is None else cfg.guidance_schedule[i]
+        lat = backend.step_windows(lat, gathered, unit_rows, frames, g, sigmas[i], sigmas[i + 1])
         shift = (shift + cfg.shift_offset) % F
         if step_callback is not None:
             step_callback(i)

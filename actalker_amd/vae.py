@@ -393,6 +393,36 @@ class AutoencoderKLTemporalDecoder(nn.Module):
         self.decoder = TemporalDecoder(latent_channels, out_channels, block_out_channels, layers_per_block)
         self.quant_conv = Conv2d(2 * latent_channels, 2 * latent_channels, 1)
 
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path, subfolder: Optional[str] = None,
+                        variant: Optional[str] = None, **kwargs):
+        """Local diffusers folder loader (config.json + safetensors / bin weights, strict), as
+        ``AutoencoderKLTemporalDecoder.from_pretrained(path, subfolder="vae", variant="fp16")``
+        (Inference.py:41-44). Weights are read with safetensors or torch.load(weights_only=True)."""
+        import json
+        import os
+        root = pretrained_model_name_or_path if subfolder is None else os.path.join(pretrained_model_name_or_path,
+                                                                                      subfolder)
+        if not os.path.isdir(root):
+            raise OSError(f"{root} is not a local directory (no network access in this build)")
+        with open(os.path.join(root, "config.json")) as f:
+            cfg = {k: v for k, v in json.load(f).items() if not k.startswith("_")}
+        model = cls(**cfg)
+        stem = "diffusion_pytorch_model"
+        names = ([f"{stem}.{variant}.safetensors", f"{stem}.{variant}.bin"] if variant else []) + \
+                [f"{stem}.safetensors", f"{stem}.bin"]
+        for n in names:
+            p = os.path.join(root, n)
+            if os.path.exists(p):
+                if p.endswith(".safetensors"):
+                    from safetensors.torch import load_file
+                    sd = load_file(p)
+                else:
+                    sd = torch.load(p, map_location="cpu", weights_only=True)
+                model.load_state_dict(sd, strict=True)
+                return model
+        raise OSError(f"no weights found in {root}")
+
     @property
     def dtype(self):
         return self.decoder.conv_in.weight.dtype

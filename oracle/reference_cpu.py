@@ -568,7 +568,7 @@ def denoise_loop(unet_fn, latents_all, image_latents, image_embeddings, audio_pr
     """Pose2VideoLongSVDPipeline.__call__ step x window loop (pipeline_svd_audio_adapter_motionexp_idembed_
     vasa_two_ip.py:670-756). Tensor shapes are the pipeline's after CFG stacking:
       latents_all (1, T, 4, h, w), image_latents (4, T, 4, h, w), image_embeddings (4, T, 1, 1024),
-      audio_prompts (4, T, 32, 1024), vasa_prompts (4, T, 1, 1024), pose_fea (1, T, 320, h, w), T = N + fpb.
+      audio_prompts (4, T, 32, 1024), vasa_prompts (4, T, 1, 1024), pose_fea (1, N or T, 320, h, w), T = N + fpb.
     unet_fn(sample, t, ehs, added_time_ids, spatial_condition, cak) -> (4, fpb, 4, h, w)."""
     sigmas, timesteps = euler_karras_tables(num_inference_steps, sigma_min, sigma_max)
     g1, g2, g3 = guidance
@@ -581,7 +581,10 @@ def denoise_loop(unet_fn, latents_all, image_latents, image_embeddings, audio_pr
             index_start -= shift
             idx_list = [(j % T) for j in range(index_start, index_start + frames_per_batch)]
             lat = latents_all[:, idx_list]
-            pose = pose_fea[:, idx_list].repeat(4, 1, 1, 1, 1)
+            # indice_slice wraps every tensor by its OWN frame count (pipeline:687-693): pose_fea has the
+            # N pose frames, everything else T = N + fpb
+            pose = pose_fea[:, [j % pose_fea.shape[1] for j in range(index_start, index_start + frames_per_batch)]]
+            pose = pose.repeat(4, 1, 1, 1, 1)
             img = image_latents[:, idx_list]
             ide = image_embeddings[:, idx_list]
             aud = audio_prompts[:, idx_list]

@@ -158,7 +158,35 @@ static void ln_launch(const ActhLayerNormDesc* d, int cpl, hipStream_t stream) {
   }
 }
 
+// widths that are not a multiple of 8 (VasaProjModel's 1018-wide output, audio_proj.py:147-150):
+// one wave per row, scalar bf16 loads, two-pass mean / variance from registers-free re-reads
+__global__ __launch_bounds__(256) void layernorm_scalar_kernel(const ActhLayerNormDesc p) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.M) return;
+  const bf16_t* x = (const bf16_t*)p.x + row * p.ldx;
+  float s = 0.0f;
+  for (int c = lane; c < p.C; c += 64) s += bf2f(x[c]);
+  const float mean = wave_sum(s) / p.C;
+  float q = 0.0f;
+  for (int c = lane; c < p.C; c += 64) { const float d = bf2f(x[c]) - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / p.C + p.eps);
+  bf16_t* y = (bf16_t*)p.y + row * p.ldy;
+  for (int c = lane; c < p.C; c += 64) {
+    float o = (bf2f(x[c]) - mean) * rstd;
+    if (p.gamma) o = o * p.gamma[c] + (p.beta ? p.beta[c] : 0.0f);
+    y[c] = f2bf(o);
+  }
+}
+
 extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
+  if (d && d->x && d->y && d->C > 0 && (d->C % 8 || d->ldx % 8 || d->ldy % 8) && !d->add && !d->sum_out &&
+      d->ldx >= d->C && d->ldy >= d->C) {
+    if (d->M == 0) return ACTH_OK;
+    hipLaunchKernelGGL(layernorm_scalar_kernel, dim3((unsigned)((d->M + 3) / 4)), dim3(256), 0, stream, *d);
+    ACTH_CHECK_LAUNCH();
+    return ACTH_OK;
+  }
   if (!d || !d->x || !d->y || d->C <= 0 || d->C % 8 || d->C > 64 * 8 * MAXCH) return ACTH_EINVAL;
   if (d->ldx % 8 || d->ldy % 8 || (d->add && (d->ldadd % 8 || d->add_div <= 0)) || (d->sum_out && d->ldsum % 8))
     return ACTH_EINVAL;

@@ -134,6 +134,19 @@ def test_conv_direct_kernel_vs_torch(dev):
 
 
 @pytest.mark.gpu
+def test_vasa_proj_1018_wide(dev):
+    """VasaProjModel(512, vasa_expression_dim=1018) as Inference.py:78 builds it (width % 8 != 0)."""
+    from actalker_amd.adapters import VasaProjModel
+    m = VasaProjModel(512, 1018)
+    sd = synthetic_state_dict(36, {k: tuple(v.shape) for k, v in m.state_dict().items()})
+    m.load_state_dict(sd)
+    x = torch.randn(5, 512, generator=torch.Generator().manual_seed(8))
+    y = m.to(dev)(x.to(dev))
+    assert y.shape == (5, 1018)
+    assert _rel(y.cpu(), ref.vasa_proj_model(sd, "", x)) < 2e-2
+
+
+@pytest.mark.gpu
 def test_softmax_rows_vs_torch(dev):
     from actalker_amd import ops
     torch.manual_seed(1)

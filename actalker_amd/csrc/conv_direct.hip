@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(const ActhConvDirectDe
     const int co = co0 + j;
     float v = acc[j] + ((p.bias && co < p.Cout) ? p.bias[co] : 0.0f);
     if (p.act == 1) v = silu_f(v);
+    else if (p.act == 3) v = gelu_erf(v);
     acc[j] = v;
   }
   const bool full = co0 + CG <= p.Cout;
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(const ActhConvDirectDe
 extern "C" int acth_conv_direct(const ActhConvDirectDesc* d, hipStream_t stream) {
   if (!d || !d->x || !d->w || !d->y) return ACTH_EINVAL;
   if (d->Cin <= 0 || d->Cout <= 0 || d->ldx < d->Cin || d->ldy < d->Cout) return ACTH_EINVAL;
-  if (d->act != 0 && d->act != 1) return ACTH_EINVAL;
+  if (d->act != 0 && d->act != 1 && d->act != 3) return ACTH_EINVAL;
   long long Mout;
   if (d->mode == 0) {
     if (d->B <= 0 || d->H <= 0 || d->W <= 0 || (d->stride != 1 && d->stride != 2)) return ACTH_EINVAL;

@@ -150,7 +150,8 @@ size_t acth_selective_scan_workspace_size(int nb, int G, int D, int nchunks);
  * (PoseGuider InflatedConv3d, pose_guider.py:17-73; VAE Encoder conv_in / downsamplers, TemporalDecoder
  * conv_in / conv_out / time_conv_out).
  * x: NHWC bf16 rows; w: fp32 (taps*Cin, Cout), k = tap*Cin + c (tap = ky*3 + kx, or the frame tap);
- * y: rows (B*Ho*Wo | B*F*S, ldy), bf16 or fp32; act 0 none / 1 silu */
+ * y: rows (B*Ho*Wo | B*F*S, ldy), bf16 or fp32; act 0 none / 1 silu / 3 gelu (erf).
+ * A Conv1d (k 3, pad 1, stride s) is the H = 1 case with the kernel in the middle row (Whisper conv1/conv2). */
 typedef struct ActhConvDirectDesc {
   const void* x; int ldx;
   const float* w; const float* bias;

@@ -537,6 +537,33 @@ def vae_encode_moments(sd: SD, x, p: str = "encoder", n_down: int = 4, layers_pe
     return F.conv2d(x, sd["quant_conv.weight"], sd["quant_conv.bias"])
 
 
+# ============================================================================ Whisper-tiny encoder
+def whisper_encoder_hidden_states(sd: SD, x, heads: int = 6, n_layers: int = 4):
+    """transformers WhisperEncoder (4.40.2, requirements.txt:11; called at Inference.py:453) with
+    output_hidden_states: (input of every layer, final LayerNorm output)."""
+    h = F.gelu(F.conv1d(x, sd["conv1.weight"], sd["conv1.bias"], padding=1))
+    h = F.gelu(F.conv1d(h, sd["conv2.weight"], sd["conv2.bias"], stride=2, padding=1)).permute(0, 2, 1)
+    h = h + sd["embed_positions.weight"][:h.shape[1]]
+    states = []
+    for i in range(n_layers):
+        p = f"layers.{i}"
+        states.append(h)
+        r = h
+        n = layer_norm(sd, p + ".self_attn_layer_norm", h)
+        B, S, C = n.shape
+        hd = C // heads
+        q = (linear(sd, p + ".self_attn.q_proj", n) * hd ** -0.5).view(B, S, heads, hd).transpose(1, 2)
+        k = F.linear(n, sd[p + ".self_attn.k_proj.weight"]).view(B, S, heads, hd).transpose(1, 2)
+        v = linear(sd, p + ".self_attn.v_proj", n).view(B, S, heads, hd).transpose(1, 2)
+        a = torch.softmax(q @ k.transpose(-1, -2), -1) @ v
+        h = r + linear(sd, p + ".self_attn.out_proj", a.transpose(1, 2).reshape(B, S, C))
+        r = h
+        f = F.gelu(linear(sd, p + ".fc1", layer_norm(sd, p + ".final_layer_norm", h)))
+        h = r + linear(sd, p + ".fc2", f)
+    states.append(layer_norm(sd, "layer_norm", h))
+    return tuple(states)
+
+
 # ============================================================================ scheduler + loop
 def euler_karras_tables(num_inference_steps: int = 25, sigma_min: float = 0.002, sigma_max: float = 700.0,
                         rho: float = 7.0):

@@ -23,26 +23,53 @@ using namespace gemm;
 
 namespace {
 
+// A row's source coordinates packed into two registers (four rows per wave stay live across the whole
+// K loop; the unpacked RowInfo + row index form made the conv instantiation spill 12 VGPRs, and the
+// scratch reloads at every tap change waited out the in-flight LDS-DMA with them):
+//   amode 0: a = row (-1 past M);  amode 1: a = (y << 16) | x, b = image (-1 past M);
+//   amode 2: a = row (-1 past M), b = frame.
+struct RowPk { int a, b; };
+
 template <int AMODE>
-__device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, int m, const RowInfo& ri, int tap) {
-  if (!ri.ok) return -1;
-  if (AMODE == 0) return m;
+__device__ __forceinline__ RowPk pack_row(const ActhGemmDesc& p, int m) {
+  const RowInfo ri = row_info(p, m);
+  RowPk r;
   if (AMODE == 1) {
+    r.a = (ri.y << 16) | ri.x;
+    r.b = ri.ok ? ri.b : -1;
+  } else {
+    r.a = ri.ok ? m : -1;
+    r.b = ri.y;
+  }
+  return r;
+}
+
+template <int AMODE>
+__device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, const RowPk& rin, int tap) {
+  // opaque copies: without them LICM hoists y*stride / b*H products of all four rows out of the K
+  // loop, which is what pushed the conv instantiation past 256 VGPRs
+  RowPk r = rin;
+  asm volatile("" : "+v"(r.a), "+v"(r.b));
+  if (AMODE == 0) return r.a;
+  if (AMODE == 1) {
+    if (r.b < 0) return -1;
+    const int y = r.a >> 16, x = r.a & 0xffff;
     const int ky = tap / 3, kx = tap - ky * 3;
     int iy, ix;
     if (p.upsample) {
-      iy = ri.y + ky - 1; ix = ri.x + kx - 1;
+      iy = y + ky - 1; ix = x + kx - 1;
       if (iy < 0 || ix < 0 || iy >= 2 * p.H || ix >= 2 * p.W) return -1;
       iy >>= 1; ix >>= 1;
     } else {
-      iy = ri.y * p.conv_stride + ky - 1; ix = ri.x * p.conv_stride + kx - 1;
+      iy = y * p.conv_stride + ky - 1; ix = x * p.conv_stride + kx - 1;
       if (iy < 0 || ix < 0 || iy >= p.H || ix >= p.W) return -1;
     }
-    return (ri.b * p.H + iy) * p.W + ix;
+    return (r.b * p.H + iy) * p.W + ix;
   }
-  const int f = ri.y + tap - 1;
+  if (r.a < 0) return -1;
+  const int f = r.b + tap - 1;
   if (f < 0 || f >= p.F) return -1;
-  return m + (tap - 1) * p.S;
+  return r.a + (tap - 1) * p.S;
 }
 
 #define BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
@@ -102,15 +129,13 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int lrow = lane >> 3;
   const int cch = (lane & 7) ^ lrow;
   // rows [h][u]: half h, piece w + 8u
-  RowInfo ri[2][2];
-  int arow[2][2];
+  RowPk rp[2][2];
   unsigned aoff[2][2], aoff2[2][2], boff[2][NBJ];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      arow[h][u] = tile_m + h * 128 + (wave + 8 * u) * 8 + lrow;
-      ri[h][u] = row_info(p, arow[h][u]);
+      rp[h][u] = pack_row<AMODE>(p, tile_m + h * 128 + (wave + 8 * u) * 8 + lrow);
     }
 #pragma unroll
     for (int u = 0; u < NBJ; ++u) {
@@ -123,7 +148,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const int pix = tap_pixel8<AMODE>(p, arow[h][u], ri[h][u], tap);
+        const int pix = tap_pixel8<AMODE>(p, rp[h][u], tap);
         aoff[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda + cch * 8) * 2u;
         aoff2[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda2 + cch * 8) * 2u;
       }

@@ -335,9 +335,12 @@ __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTempo
     const bf16_t* base = (const bf16_t*)p.qkv + rows[it] * p.ldqkv + h * 64 + 8 * g;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      qa[it][ks] = fok ? *reinterpret_cast<const uint4*>(base + 32 * ks) : z;
-      ka[it][ks] = fok ? *reinterpret_cast<const uint4*>(base + C + 32 * ks) : z;
-      va[it][ks] = fok ? *reinterpret_cast<const uint4*>(base + 2 * C + 32 * ks) : z;
+      qa[it][ks] = z; ka[it][ks] = z; va[it][ks] = z;      // guarded loads, not `fok ? *p : z`
+      if (fok) {                                           // (that form went through a stack slot)
+        qa[it][ks] = *reinterpret_cast<const uint4*>(base + 32 * ks);
+        ka[it][ks] = *reinterpret_cast<const uint4*>(base + C + 32 * ks);
+        va[it][ks] = *reinterpret_cast<const uint4*>(base + 2 * C + 32 * ks);
+      }
     }
   }
 #pragma unroll
@@ -352,9 +355,10 @@ __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTempo
     // were issued earlier by this wave, and a wave's LDS operations complete in order
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv[ks]);
+      const uint32_t w4[4] = {vv[ks].x, vv[ks].y, vv[ks].z, vv[ks].w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) vt[(32 * ks + 8 * g + e) * TM_VLD + fr] = ve[e];
+      for (int e = 0; e < 8; ++e)
+        vt[(32 * ks + 8 * g + e) * TM_VLD + fr] = (bf16_t)(e & 1 ? w4[e >> 1] >> 16 : w4[e >> 1] & 0xffffu);
     }
     f32x4_t st = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll

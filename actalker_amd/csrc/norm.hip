@@ -430,10 +430,14 @@ __global__ __launch_bounds__(256) void mamba_combine_kernel(const ActhMambaCombi
     const int ch = gl + LPR * i;
     const bool c_ok = ok && ch < nch;
     const uint4 z = make_uint4(0, 0, 0, 0);
-    ra0[i] = c_ok ? *reinterpret_cast<const uint4*>(a0 + ch * 8) : z;
-    ra1[i] = (c_ok && a1) ? *reinterpret_cast<const uint4*>(a1 + ch * 8) : z;
-    re0[i] = c_ok ? *reinterpret_cast<const uint4*>(e0 + ch * 8) : z;
-    re1[i] = (c_ok && e1) ? *reinterpret_cast<const uint4*>(e1 + ch * 8) : z;
+    // plain guarded loads: the `cond ? *p : z` form was lowered through a private stack slot
+    ra0[i] = z; ra1[i] = z; re0[i] = z; re1[i] = z;
+    if (c_ok) {
+      ra0[i] = *reinterpret_cast<const uint4*>(a0 + ch * 8);
+      re0[i] = *reinterpret_cast<const uint4*>(e0 + ch * 8);
+      if (a1) ra1[i] = *reinterpret_cast<const uint4*>(a1 + ch * 8);
+      if (e1) re1[i] = *reinterpret_cast<const uint4*>(e1 + ch * 8);
+    }
   }
   float v[CPL][8];
   float s = 0.0f;

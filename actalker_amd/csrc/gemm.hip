@@ -184,7 +184,7 @@ int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2
 // kernel for GEGLU (its wave tiles hold whole hidden|gate granule pairs), the persistent 256x160
 // kernel for grids too small for either, the 128x128 kernel for small M or N.
 static int choose_tile(const ActhGemmDesc* d) {
-  if (d->tile) return d->tile & 0xff;
+  if (d->tile & 0xff) return d->tile & 0xff;
   if (d->N < 128 || d->M < 256) return 1;
   const long long mt = (d->M + 255) / 256;
   if (d->act == 2) return (d->N % 256 == 0 && mt * (d->N / 256) >= 256) ? 4 : 1;

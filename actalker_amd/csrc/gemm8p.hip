@@ -117,8 +117,24 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int bid = blockIdx.x + gridDim.x * blockIdx.y;
   const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
   const int lin = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-  const int tile_n = (lin % ntn) * BN_;
-  const int tile_m = (lin / ntn) * 256;
+  // Optional M-grouped raster (tile bits 16-23 = gm > 1): inside a run, gm row blocks x all N tiles
+  // with m fastest, so the ~32 tiles an XCD holds at once share gm A panels and a few B tiles
+  // instead of streaming the whole B (> 4 MB L2 for the wide GEGLU weights) per row block.
+  const int gm = (p.tile >> 16) & 0xff;
+  int tn_idx, tm_idx;
+  if (gm > 1) {
+    const int g = lin / (gm * ntn);
+    const int m0 = g * gm;
+    const int gcur = min(gm, (int)gridDim.y - m0);
+    const int r = lin - g * gm * ntn;
+    tn_idx = r / gcur;
+    tm_idx = m0 + (r - tn_idx * gcur);
+  } else {
+    tn_idx = lin % ntn;
+    tm_idx = lin / ntn;
+  }
+  const int tile_n = tn_idx * BN_;
+  const int tile_m = tm_idx * 256;
 
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
   const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(p.A2 ? p.A2 : p.A, p.A2 ? a2_bytes : 0u);
@@ -422,15 +438,27 @@ static void launch8p(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigne
     hipLaunchKernelGGL((gemm8p_kernel<BN_, 0>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
 }
 
+// Row-block group of the M-grouped raster: explicit in tile bits 16-23 (bench / tests), else
+// 8 for B operands larger than an XCD's 4 MB L2 and 0 (plain n-fastest runs) otherwise.
+static int gemm8p_group_m(const ActhGemmDesc* d) {
+  const int g = (d->tile >> 16) & 0xff;
+  if (g) return g;
+  // measured (tools/bench_gemm.py --flags): gm = 8 lifts the level-1 / level-2 GEGLU shapes
+  // (B = 6.5 / 26 MB) 3.8 / 4.6 % and the level-1 conv (7.4 MB) 1.6 %; L2-resident B: +-1 % noise
+  return (long long)d->N * d->K * 2 > (4ll << 20) ? 8 : 0;
+}
+
 // tile 4: 256 x 256; tile 5: 256 x 320 (no GEGLU: its wave column shares are not granule pairs)
 int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                   int vec_ok, hipStream_t stream) {
   const int mt = (d->M + 255) / 256;
   if (mt > 65535) return ACTH_EINVAL;
+  ActhGemmDesc dd = *d;
+  dd.tile = (d->tile & 0xffff) | (gemm8p_group_m(d) << 16);
   if (tile == 4) {
-    launch8p<256>(d, dim3((d->N + 255) / 256, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+    launch8p<256>(&dd, dim3((d->N + 255) / 256, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
   } else if (tile == 5 && d->act != 2) {
-    launch8p<320>(d, dim3((d->N + 319) / 320, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+    launch8p<320>(&dd, dim3((d->N + 319) / 320, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
   } else {
     return ACTH_EINVAL;
   }

@@ -53,23 +53,29 @@ def window_frames(T: int, fpb: int, overlap: int, shift: int) -> List[List[int]]
     return [[r % T for r in win] for win in window_frames_raw(T, fpb, overlap, shift)]
 
 
-def assign_units(n_windows: int, world: int, rank: int, n_branch: int = 4) -> Tuple[List[Tuple[int, int]], int]:
+def assign_units(n_windows: int, world: int, rank: int, n_branch: int = 4,
+                 branches: Optional[Sequence[int]] = None) -> Tuple[List[Tuple[int, int]], int]:
     """Contiguous block of (window, branch) units for ``rank``; also returns the per-rank capacity
-    (max units on any rank) used to size the all-gather."""
-    n = n_windows * n_branch
+    (max units on any rank) used to size the all-gather. ``branches``: the CFG branches evaluated
+    (default all ``n_branch``); a branch whose inputs duplicate another's is left out (see
+    ``HipBackend.branch_twins``)."""
+    br = list(range(n_branch)) if branches is None else list(branches)
+    nb = len(br)
+    n = n_windows * nb
     cap = math.ceil(n / world)
     base, extra = divmod(n, world)
     start = rank * base + min(rank, extra)
     count = base + (1 if rank < extra else 0)
-    units = [(u // n_branch, u % n_branch) for u in range(start, start + count)]
+    units = [(u // nb, br[u % nb]) for u in range(start, start + count)]
     return units, cap
 
 
-def unit_owner(n_windows: int, world: int, n_branch: int = 4) -> List[Tuple[int, int]]:
-    """For every global unit u = window*n_branch + branch: (rank, slot within that rank)."""
+def unit_owner(n_windows: int, world: int, n_branch: int = 4,
+               branches: Optional[Sequence[int]] = None) -> List[Tuple[int, int]]:
+    """For every global unit u = window*len(branches) + branch position: (rank, slot within that rank)."""
     owners = []
     for r in range(world):
-        units, _ = assign_units(n_windows, world, r, n_branch)
+        units, _ = assign_units(n_windows, world, r, n_branch, branches)
         for slot, (w, c) in enumerate(units):
             owners.append((r, slot))
     return owners
@@ -116,6 +122,29 @@ class HipBackend:
         self.pose_P = pose_fea.shape[1]
         self._raw = None
         self.added = added_time_ids.to(dev, torch.float32)                                          # (nb, 3)
+
+    def branch_twins(self) -> dict:
+        """{branch: earlier branch with bitwise-identical UNet inputs}. The 4 CFG branches
+        (pipeline:162-200: uncond, drop audio+vasa, drop vasa, cond) differ only in the ID embedding,
+        image latents and the gated audio / VASA prompts (pipeline:724). Under gate [1, 0] (mode 0)
+        every VASA prompt is multiplied by 0, so "drop vasa" and "cond" receive identical inputs;
+        under gate [0, 1] (mode 1) the audio prompts vanish and "drop audio+vasa" equals "drop vasa".
+        The UNet treats batch elements independently and every kernel is deterministic, so such a
+        branch's noise prediction is bitwise the twin's: it is evaluated once and read twice by
+        guidance (whose g3 / g2 term is then exactly zero, as in the reference)."""
+        nb = self.ide.shape[0]
+        img = self.img.reshape(nb, -1)
+        twins = {}
+        for c in range(1, nb):
+            for e in range(c):
+                if e in twins:
+                    continue
+                if (torch.equal(self.ide[c], self.ide[e]) and torch.equal(img[c], img[e])
+                        and torch.equal(self.aud[c], self.aud[e]) and torch.equal(self.vas[c], self.vas[e])
+                        and torch.equal(self.added[c], self.added[e])):
+                    twins[c] = e
+                    break
+        return twins
 
     def begin_step(self, raw_frames: List[List[int]]):
         self._raw = raw_frames
@@ -183,6 +212,8 @@ class LoopConfig:
     # (2 calls per step), two streams ran 0.5 % slower (the GEMM / attention blocks occupy every
     # CU's registers or LDS, so kernels of the two calls cannot co-reside)
     concurrent_calls: int = 1
+    # evaluate a CFG branch whose inputs are bitwise those of another branch once (backend.branch_twins)
+    dedup_branches: bool = True
 
 
 def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, world: int = 1,
@@ -196,8 +227,10 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
     sigmas, timesteps = karras_sigmas(cfg.num_inference_steps, cfg.sigma_min, cfg.sigma_max)
     lat = backend.new_state(latents_all)
     n_windows = len(range(0, T, F - cfg.overlap))
-    my_units, cap = assign_units(n_windows, world, rank)
-    owners = unit_owner(n_windows, world)
+    twins = backend.branch_twins() if (cfg.dedup_branches and hasattr(backend, "branch_twins")) else {}
+    branches = [c for c in range(4) if c not in twins]
+    my_units, cap = assign_units(n_windows, world, rank, branches=branches)
+    owners = unit_owner(n_windows, world, branches=branches)
     S = backend.S
     rows_per_unit = F * S
     local = torch.zeros((cap * rows_per_unit, 4), device=lat.device, dtype=torch.float32)
@@ -232,7 +265,8 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
         if world > 1:
             import torch.distributed as dist
             dist.all_gather_into_tensor(gathered, local, group=group)
-        unit_rows = [[unit_row[w * 4 + c] for c in range(4)] for w in range(n_windows)]
+        pos = {c: branches.index(twins.get(c, c)) for c in range(4)}
+        unit_rows = [[unit_row[w * len(branches) + pos[c]] for c in range(4)] for w in range(n_windows)]
         g = cfg.guidance if cfg.guidance_schedule is None else cfg.guidance_schedule[i]
         lat = backend.step_windows(lat, gathered, unit_rows, frames, g, sigmas[i], sigmas[i + 1])
         shift = (shift + cfg.shift_offset) % F

@@ -5,7 +5,11 @@ per GPU (BASELINE.json metric), on 1..8 MI355X with one process per GPU.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
 
 A "step" is one sampler step of the loop (pipeline:671): every window x CFG-branch UNet pass
-(2 x 56-frame calls at N=14 on one GPU) + guidance + Euler + window accumulation. The sampler's
+(2 x 56-frame calls at N=14 on one GPU) + guidance + Euler + window accumulation. In modes 0 / 1 the
+gate zeroes the VASA / audio prompts (pipeline:724), so two of the four CFG branches receive
+bitwise-identical inputs; that branch is evaluated once and read twice by guidance (identical
+output; pipeline.HipBackend.branch_twins), i.e. 3 x 14-frame UNet batches per window. --no-dedup
+evaluates all four, as the reference does. The sampler's
 steps are shape-identical, so frames/sec = N_frames / (25 * seconds_per_step). Weak scaling: each GPU
 adds 14 output frames (N = 14 * world), units = (window, CFG branch) sharded contiguously, one RCCL
 all-gather of noise predictions per step.
@@ -218,6 +222,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-dedup", action="store_true",
+                    help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
+    ap.add_argument("--units-per-call", type=int, default=4,
+                    help="(window, branch) units per UNet call (4 = the reference's 56-frame call)")
     ap.add_argument("--concurrent-calls", type=int, default=1,
                     help="run a rank's independent UNet calls of a step on this many HIP streams")
     args = ap.parse_args()
@@ -249,7 +257,11 @@ def main():
                             inp["image_latents"], inp["image_embeddings"], inp["audio_prompts"],
                             inp["vasa_prompts"], inp["pose_fea"])
     cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7,
-                        concurrent_calls=args.concurrent_calls)
+                        concurrent_calls=args.concurrent_calls, dedup_branches=not args.no_dedup,
+                        units_per_call=args.units_per_call)
+    twins = backend.branch_twins() if cfg.dedup_branches else {}
+    branches = [c for c in range(4) if c not in twins]
+    log(f"CFG branches evaluated: {branches} (twins {twins})")
 
     def barrier():
         if world > 1:
@@ -295,7 +307,7 @@ def main():
                     launches=timer.launches, avg_launch_us=round(1000.0 * gemm_ms / timer.launches, 2),
                     flop_per_launch=round(timer.flops / timer.launches),
                     kernel_share_of_step=round(gemm_ms / (elapsed * 1000.0), 3))
-    n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank)[0])
+    n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank, branches=branches)[0])
     frame_fwds = n_units_rank * fpb * args.steps
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -307,11 +319,15 @@ def main():
             "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"workload": f"{mode_name}, {H}x{W}, {N} frames ({args.frames_per_gpu}/GPU), fpb {fpb}, "
-                                   f"25-step EulerDiscrete, 4-way CFG, (window x branch) units over {world} GPU(s)",
+                                   f"25-step EulerDiscrete, 4-way CFG ({len(branches)} distinct branch inputs evaluated"
+                                   + (f", branch {sorted(twins)} = twin {[twins[k] for k in sorted(twins)]} under gate "
+                                      f"{gate}" if twins else "")
+                                   + f"), (window x branch) units over {world} GPU(s)",
                        "model": "SVD-XT UNet + ACTalker v10 dual-Mamba (1.775B, random init)",
                        "global_batch": N, "seq_len": fpb, "parallelism": f"units{world}"},
             "unet_frame_forwards_per_s_per_gpu": round(frame_fwds / elapsed, 3),
             "achieved_mfma_tflops_whole_step": round(frame_fwds * TFLOP_PER_FRAME_FWD / elapsed, 1),
+            "cfg_branches_evaluated": len(branches),
             "finite": ok,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -51,7 +51,7 @@ typedef struct ActhGemmDesc {
   int out_f32;
   void* C; int ldc;
   int orow_div, orow_stride, orow_off;
-  int tile;                  /* 0 auto; 1 128x128 (4 waves); 2 256x256, 3 256x160, 4 256x256 / 5 256x320 phased (8 waves) */
+  int tile;                  /* bits 0-7: 0 auto; 1 128x128 (4 waves); 2 256x256, 3 256x160, 4 256x256 / 5 256x320 phased (8 waves); bits 16-23: row-block group of the phased kernels' tile order (0 auto) */
 } ActhGemmDesc;
 int acth_gemm(const ActhGemmDesc* d, hipStream_t stream);
 int acth_gemm_desc_size(void);

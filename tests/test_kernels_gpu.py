@@ -94,6 +94,26 @@ def test_gemm_geglu_and_orow(dev):
     assert float(got[0:3].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("tile", [4, 5])
+@pytest.mark.parametrize("gm", [1, 3, 8])
+def test_gemm_grouped_raster(dev, tile, gm):
+    """M-grouped tile order of the phased kernels (tile bits 16-23): every (m, n) tile written once,
+    including the partial last group (11 row blocks over groups of 3 / 8) and a ragged N."""
+    from actalker_amd.modules import pack_geglu
+    M, N, K = 11 * 256 - 40, 1280 + 64, 192
+    a, w = bf(rnd(M, K)), bf(rnd(N, K, scale=K ** -0.5))
+    bias = rnd(N)
+    if tile == 4:
+        wp, bp = pack_geglu(rnd(2 * 640, K, scale=K ** -0.5), rnd(2 * 640, scale=0.1))
+        out = ops.gemm(a.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile | (gm << 16))
+        ref0 = ops.gemm(a.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile)
+        assert torch.equal(out, ref0)
+    else:
+        out = ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), tile=tile | (gm << 16))
+        assert rel(out, a.float() @ w.float().t() + bias) < 1e-2
+        assert torch.equal(out, ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), tile=tile))
+
+
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
 def test_gemm_tile_variants(dev, tile):
     """Every tile kernel (128x128; 256x256 / 256x160 8-wave; phased 256x256 / 256x320) on all A

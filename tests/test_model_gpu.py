@@ -126,6 +126,57 @@ def test_pipeline_loop_matches_oracle(dev, tiny):
     assert err < 5e-2, err
 
 
+@pytest.mark.parametrize("gate,twins", [([1, 0], {3: 2}), ([0, 1], {2: 1})])
+def test_pipeline_loop_twin_branches(dev, tiny, gate, twins):
+    """Modes 0 / 1 with the pipeline's CFG stacking (ID [0,e,e,e], audio [u,u,a,a], VASA [u,u,u,v],
+    pipeline:162-200, prompts gated at :724): the backend finds the twin branch, the loop evaluates
+    3 branches per window and still matches the 4-branch oracle loop (and the 4-branch HIP loop)."""
+    from actalker_amd import pipeline as pl
+    unet, sd, cfg = tiny
+    N, fpb, H, W = 4, 2, 16, 32
+    T = N + fpb
+    g = torch.Generator().manual_seed(23)
+    latents = 0.18215 * torch.randn(1, 1, 4, H, W, generator=g) + 700.0 * torch.randn(1, T, 4, H, W, generator=g)
+    il = torch.randn(1, T, 4, H, W, generator=g)
+    imgl = torch.cat([torch.zeros_like(il), il, il, il])
+    e = torch.randn(1, T, 1, 1024, generator=g)
+    ide = torch.cat([torch.zeros_like(e), e, e, e])
+    a_u, a_c = torch.randn(1, T, 32, 1024, generator=g), torch.randn(1, T, 32, 1024, generator=g)
+    aud = torch.cat([a_u, a_u, a_c, a_c])
+    v_u, v_c = torch.randn(1, T, 1, 1024, generator=g), torch.randn(1, T, 1, 1024, generator=g)
+    vas = torch.cat([v_u, v_u, v_u, v_c])
+    pose = 0.1 * torch.randn(1, T, 64, H, W, generator=g)
+    added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
+    ones = torch.ones(1, 1, 8 * H, 8 * W)
+    masks = (ones, ones, ones)
+    backend = pl.HipBackend(unet, H, W, masks, gate, added, T, fpb, imgl, ide, aud, vas, pose)
+    assert backend.branch_twins() == twins
+    seen = []
+    run0 = backend.run_units
+
+    def counting(lat, units, *a, **k):
+        seen.extend(units)
+        return run0(lat, units, *a, **k)
+
+    backend.run_units = counting
+    lc = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, num_inference_steps=25)
+    with torch.no_grad():
+        got = pl.denoise(backend, latents, lc, steps=3)
+        assert len(seen) == 3 * 3 * 3 and not any(c in twins for _w, c in seen)
+        lc4 = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, num_inference_steps=25,
+                            dedup_branches=False)
+        all4 = pl.denoise(backend, latents, lc4, steps=3)
+    assert rel(got, all4) < 1e-2
+
+    def unet_fn(sample, t, ehs, added_ids, sc, cak):
+        return ref.unet_forward(sd, sample, t, ehs, added_ids, sc, cak, ip_scale=(1.25, 1.25),
+                                cfg=_oracle_cfg(cfg))
+
+    want = _oracle_loop(unet_fn, latents, imgl, ide, aud, vas, pose, added, masks, gate, N, fpb, steps=3)
+    err = rel(got, want)
+    assert err < 5e-2, err
+
+
 def _oracle_loop(unet_fn, latents, imgl, ide, aud, vas, pose, added, masks, gate, N, fpb, steps):
     """oracle.denoise_loop truncated to `steps` sampler steps (same schedule)."""
     sig, ts = ref.euler_karras_tables(25)

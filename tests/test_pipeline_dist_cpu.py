@@ -68,6 +68,24 @@ class CpuBackend:
         return lat
 
 
+class TwinCpuBackend(CpuBackend):
+    """Mode-0-like conditioning: branch 3 ("cond") receives exactly branch 2's inputs ("drop vasa",
+    VASA prompts gated to zero), so its stand-in noise is branch 2's."""
+
+    COND = (0, 1, 2, 2)
+
+    def run_units(self, lat, units, frames, t, sigma, out, row0):
+        F, S = self.F, self.S
+        for u, (wdx, c) in enumerate(units):
+            idx = frames[wdx]
+            x = torch.cat([lat[0, idx] / math.sqrt(sigma * sigma + 1.0), self.img[c, idx]], dim=1)
+            noise = fake_unet(x, self.COND[c], t)
+            out[row0 + u * F * S: row0 + (u + 1) * F * S] = noise.permute(0, 2, 3, 1).reshape(-1, 4)
+
+    def branch_twins(self):
+        return {3: 2}
+
+
 def oracle_loop(latents, imgl, N, fpb, shift_offset, steps):
     sig, ts = ref.euler_karras_tables(25)
     T = N + fpb
@@ -107,13 +125,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, N, fpb, steps, q):
+def _worker(rank, world, port, N, fpb, steps, q, twin=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         latents, imgl = make_case(N, fpb)
-        backend = CpuBackend(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
+        if twin:
+            imgl[3] = imgl[2]
+        backend = (TwinCpuBackend if twin else CpuBackend)(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
         cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1, units_per_call=2)
         out = pl.denoise(backend, latents, cfg, rank, world, steps=steps)
         q.put((rank, out))
@@ -173,3 +193,55 @@ def test_sharded_loop_matches_single_process(world):
     # every rank holds the identical latent state (replicated guidance/Euler)
     for r in range(1, world):
         assert torch.equal(outs[r], outs[0])
+
+
+def test_unit_assignment_with_deduplicated_branch():
+    """Branches [0, 1, 2] (mode 0: branch 3 is branch 2's twin): N = 112 -> 27 units over 8 GPUs."""
+    for n_windows, world in ((2, 1), (9, 8), (3, 2)):
+        seen = []
+        for r in range(world):
+            units, cap = pl.assign_units(n_windows, world, r, branches=[0, 1, 2])
+            assert len(units) <= cap
+            seen += units
+        assert sorted(seen) == [(w, c) for w in range(n_windows) for c in range(3)]
+    assert [len(pl.assign_units(9, 8, r, branches=[0, 1, 2])[0]) for r in range(8)] == [4, 4, 4, 3, 3, 3, 3, 3]
+    assert pl.assign_units(2, 1, 0, branches=[0, 2, 3])[0] == [(0, 0), (0, 2), (0, 3), (1, 0), (1, 2), (1, 3)]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_twin_branch_evaluated_once_matches_four_branch_loop(world):
+    """Dedup (3 branches evaluated, branch 3 read from branch 2's rows) == all 4 evaluated, exactly,
+    on 1 process and on 2 gloo ranks."""
+    N, fpb, steps = 6, 3, 3
+    latents, imgl = make_case(N, fpb)
+    imgl[3] = imgl[2]
+    calls = []
+
+    class Counting(TwinCpuBackend):
+        def run_units(self, lat, units, frames, t, sigma, out, row0):
+            calls.extend(units)
+            super().run_units(lat, units, frames, t, sigma, out, row0)
+
+    cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1, units_per_call=2)
+    b4 = Counting(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
+    want = pl.denoise(b4, latents, pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1,
+                                                 units_per_call=2, dedup_branches=False), steps=steps)
+    assert len(calls) == 3 * 4 * steps
+    calls.clear()
+    if world == 1:
+        got = pl.denoise(Counting(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb), latents, cfg, steps=steps)
+        assert len(calls) == 3 * 3 * steps and all(c != 3 for _w, c in calls)
+        assert torch.equal(got, want)
+        return
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        torch.testing.assert_close(outs[r], want, rtol=0, atol=0)

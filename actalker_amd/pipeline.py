@@ -9,8 +9,8 @@ Work decomposition. Within a step every window is independent (overlap = 0 gives
 sets, pipeline:684-751) and so is every CFG branch until guidance (:731-733). A *unit* is one
 (window, CFG branch) pair = one 14-frame UNet batch element. Units are dealt to ranks in contiguous
 blocks (N = 112 -> 9 windows x 4 branches = 36 units -> 5/5/5/5/4/4/4/4 over 8 GPUs); each rank runs
-its units in UNet calls of up to ``units_per_call`` units (4 = one 56-frame batch, the reference's
-call shape), then ONE all-gather of the fp32 noise predictions per step (RCCL over xGMI; torch's
+its units in as few UNet calls as the kernels' buffer extents allow (6 x 14 frames at 576x1024; the
+reference's call is 4 units = 56 frames), then ONE all-gather of the fp32 noise predictions per step (RCCL over xGMI; torch's
 "nccl" backend is RCCL on ROCm) gives every rank all branches, and every rank applies guidance +
 Euler + window accumulation for all windows (tiny, replicated) so the latent state stays identical
 everywhere without a second collective. Frames of one window never split across ranks (temporal
@@ -81,6 +81,21 @@ def unit_owner(n_windows: int, world: int, n_branch: int = 4,
     return owners
 
 
+def call_splits(n_units: int, max_per_call: int) -> List[Tuple[int, int]]:
+    """[start, end) unit ranges: the fewest UNet calls of at most ``max_per_call`` units, sizes
+    differing by at most one (5 units, max 4 -> 3 + 2 rather than 4 + 1)."""
+    if n_units <= 0:
+        return []
+    n_calls = -(-n_units // max(1, max_per_call))
+    base, extra = divmod(n_units, n_calls)
+    out, c0 = [], 0
+    for i in range(n_calls):
+        c1 = c0 + base + (1 if i < extra else 0)
+        out.append((c0, c1))
+        c0 = c1
+    return out
+
+
 def gate_masks(gate, face_mask: torch.Tensor, mouth_mask: torch.Tensor, exp_mask: torch.Tensor):
     """ip_adapter_masks for a gate (pipeline:702-711): [1,1] -> [mouth, exp]; [1,0] -> [face, 0];
     [0,1] -> [0, face]."""
@@ -122,6 +137,14 @@ class HipBackend:
         self.pose_P = pose_fea.shape[1]
         self._raw = None
         self.added = added_time_ids.to(dev, torch.float32)                                          # (nb, 3)
+
+    def max_units_per_call(self) -> int:
+        """Largest UNet call (in 14-frame units) whose widest activation stays under the kernels'
+        2 GiB buffer extent (32-bit buffer offsets): level-0 rows x 4*C0 bf16 (the GEGLU hidden and
+        the Mamba xz rows). 576x1024, C0 = 320: 91 frames -> 6 units."""
+        c0 = int(self.unet.config.block_out_channels[0])
+        per_unit = self.F * self.S * 4 * c0 * 2
+        return max(1, (2 ** 31 - 1) // per_unit)
 
     def branch_twins(self) -> dict:
         """{branch: earlier branch with bitwise-identical UNet inputs}. The 4 CFG branches
@@ -206,7 +229,11 @@ class LoopConfig:
     guidance_schedule: Optional[List[Tuple[float, float, float]]] = None
     sigma_min: float = 0.002
     sigma_max: float = 700.0
-    units_per_call: int = 4
+    # (window, branch) units per UNet call; 0 = auto: the fewest calls the backend's size limit
+    # allows (backend.max_units_per_call), split evenly. Measured on MI355X, mode 0 at N = 14
+    # (6 units per step): one 84-frame call 406.8 ms/step vs 4 + 2 units 444.0 ms, 3 + 3 430.1 ms
+    # (profiles/r1_step11_bench.log, profiles/r1_step12_bench_upc{3,6}.log): fewer, larger launches fill the lower UNet levels better
+    units_per_call: int = 0
     # a rank's UNet calls of one step are independent (disjoint units, disjoint output rows): run up
     # to this many of them on their own HIP streams. Off by default: measured on MI355X at N = 14
     # (2 calls per step), two streams ran 0.5 % slower (the GEMM / attention blocks occupy every
@@ -240,7 +267,10 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
     unit_row = [(r * cap + slot) * rows_per_unit for (r, slot) in owners]
     shift = 0
     n_steps = cfg.num_inference_steps if steps is None else steps
-    calls = list(range(0, len(my_units), cfg.units_per_call))
+    upc = cfg.units_per_call
+    if upc <= 0:
+        upc = backend.max_units_per_call() if hasattr(backend, "max_units_per_call") else 4
+    calls = call_splits(len(my_units), upc)
     streams = []
     if cfg.concurrent_calls > 1 and len(calls) > 1 and lat.is_cuda:
         streams = [torch.cuda.Stream(device=lat.device) for _ in range(min(cfg.concurrent_calls, len(calls)))]
@@ -252,15 +282,15 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
             main = torch.cuda.current_stream(lat.device)
             for s in streams:
                 s.wait_stream(main)                  # this step's latent state is ready
-            for ci, c0 in enumerate(calls):
-                chunk = my_units[c0:c0 + cfg.units_per_call]
+            for ci, (c0, c1) in enumerate(calls):
+                chunk = my_units[c0:c1]
                 with torch.cuda.stream(streams[ci % len(streams)]):
                     backend.run_units(lat, chunk, frames, timesteps[i], sigmas[i], local, c0 * rows_per_unit)
             for s in streams:
                 main.wait_stream(s)                  # every noise row written before the gather / step
         else:
-            for c0 in calls:
-                chunk = my_units[c0:c0 + cfg.units_per_call]
+            for c0, c1 in calls:
+                chunk = my_units[c0:c1]
                 backend.run_units(lat, chunk, frames, timesteps[i], sigmas[i], local, c0 * rows_per_unit)
         if world > 1:
             import torch.distributed as dist

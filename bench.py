@@ -5,7 +5,7 @@ per GPU (BASELINE.json metric), on 1..8 MI355X with one process per GPU.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
 
 A "step" is one sampler step of the loop (pipeline:671): every window x CFG-branch UNet pass
-(2 x 56-frame calls at N=14 on one GPU) + guidance + Euler + window accumulation. In modes 0 / 1 the
+(one 84-frame call in modes 0/1, two 56-frame calls in mode 2, at N=14 on one GPU) + guidance + Euler + window accumulation. In modes 0 / 1 the
 gate zeroes the VASA / audio prompts (pipeline:724), so two of the four CFG branches receive
 bitwise-identical inputs; that branch is evaluated once and read twice by guidance (identical
 output; pipeline.HipBackend.branch_twins), i.e. 3 x 14-frame UNet batches per window. --no-dedup
@@ -224,8 +224,9 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
-    ap.add_argument("--units-per-call", type=int, default=4,
-                    help="(window, branch) units per UNet call (4 = the reference's 56-frame call)")
+    ap.add_argument("--units-per-call", type=int, default=0,
+                    help="(window, branch) units per UNet call; 0 = auto (fewest calls within the kernels' "
+                         "2 GiB buffer extents; the reference's call is 4 units = 56 frames)")
     ap.add_argument("--concurrent-calls", type=int, default=1,
                     help="run a rank's independent UNet calls of a step on this many HIP streams")
     args = ap.parse_args()

@@ -245,3 +245,38 @@ def test_twin_branch_evaluated_once_matches_four_branch_loop(world):
         assert p.exitcode == 0
     for r in range(world):
         torch.testing.assert_close(outs[r], want, rtol=0, atol=0)
+
+
+def test_call_splits_fewest_even_calls():
+    assert pl.call_splits(6, 6) == [(0, 6)]
+    assert pl.call_splits(8, 6) == [(0, 4), (4, 8)]
+    assert pl.call_splits(5, 4) == [(0, 3), (3, 5)]
+    assert pl.call_splits(1, 4) == [(0, 1)]
+    assert pl.call_splits(0, 4) == []
+    for n in range(1, 20):
+        for m in range(1, 8):
+            sp = pl.call_splits(n, m)
+            assert sp[0][0] == 0 and sp[-1][1] == n and all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
+            sizes = [b - a for a, b in sp]
+            assert max(sizes) <= m and max(sizes) - min(sizes) <= 1 and len(sp) == -(-n // m)
+
+
+def test_auto_units_per_call_uses_backend_limit():
+    """units_per_call = 0: calls sized by backend.max_units_per_call(); same result as fixed sizes."""
+    N, fpb, steps = 6, 3, 3
+    latents, imgl = make_case(N, fpb)
+    sizes = []
+
+    class Limited(CpuBackend):
+        def max_units_per_call(self):
+            return 5
+
+        def run_units(self, lat, units, frames, t, sigma, out, row0):
+            sizes.append(len(units))
+            super().run_units(lat, units, frames, t, sigma, out, row0)
+
+    b = Limited(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
+    got = pl.denoise(b, latents, pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1), steps=steps)
+    assert sizes == [4, 4, 4] * steps          # 12 units per step, at most 5 per call -> 4 + 4 + 4
+    want = oracle_loop(latents, imgl, N, fpb, 1, steps)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-3)

@@ -43,6 +43,28 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f));
 }
 
+// Two GELUs in packed f32x2 arithmetic, no transcendental: erf(z) = z * P(z^2) on z clamped to
+// [-3.3, 3.3] (erf(3.3) = 1 - 3.1e-6), P a degree-11 Chebyshev fit in z^2 evaluated by Horner with
+// v_pk_fma_f32. |erf error| <= 4.3e-5 in fp32 (|GELU error| <= 1.0e-4 at |x| ~ 4, i.e. < 1 % of a
+// bf16 ulp there), against two quarter-rate transcendentals + 7 scalar FMAs per value in gelu_erf:
+// the GEGLU epilogue of the K = 320 / 640 GEMMs is VALU-bound on this math.
+typedef float float2_pk __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float2_pk gelu_pk(float2_pk x) {
+  constexpr float c[12] = {1.128378868e+00f, -3.761171401e-01f, 1.127940044e-01f, -2.678386122e-02f,
+                           5.143333692e-03f, -8.073762292e-04f, 1.023587902e-04f, -1.013244946e-05f,
+                           7.433642963e-07f, -3.751234701e-08f, 1.150420870e-09f, -1.604821484e-11f};
+  float2_pk z = x * (float2_pk){0.70710678118654752f, 0.70710678118654752f};
+  z.x = __builtin_amdgcn_fmed3f(z.x, -3.3f, 3.3f);
+  z.y = __builtin_amdgcn_fmed3f(z.y, -3.3f, 3.3f);
+  const float2_pk u = z * z;
+  float2_pk r = {c[11], c[11]};
+#pragma unroll
+  for (int k = 10; k >= 0; --k) r = __builtin_elementwise_fma(r, u, (float2_pk){c[k], c[k]});
+  const float2_pk hx = x * (float2_pk){0.5f, 0.5f};
+  return __builtin_elementwise_fma(hx, z * r, hx);
+}
+
 __device__ __forceinline__ float softplus_f(float x) {
   // torch.nn.functional.softplus(beta=1, threshold=20)
   return x > 20.0f ? x : log1pf(__expf(x));

@@ -375,7 +375,12 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
           for (int e = 0; e < 8; ++e) {
             h[e] = hs[e] * p.alpha + sbias[lc0 + oc + e];
             gt[e] = gs[e] * p.alpha + sbias[lc0 + 16 + oc + e];
-            v[e] = h[e] * gelu_erf(gt[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            const float2_pk gg = gelu_pk((float2_pk){gt[e], gt[e + 1]});
+            v[e] = h[e] * gg.x;
+            v[e + 1] = h[e + 1] * gg.y;
           }
           store8(p, out_row(p, row0 + r), col0 / 2 + oc, v, true, vec_ok);
         }

@@ -249,7 +249,11 @@ __device__ __forceinline__ void epilogue_geglu8(const ActhGemmDesc& p, int row, 
     add8(gv, p.bias + gcol, !((size_t)(p.bias + gcol) & 15), 8);
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = hv[e] * gelu_erf(gv[e]);
+  for (int e = 0; e < 8; e += 2) {
+    const float2_pk gg = gelu_pk((float2_pk){gv[e], gv[e + 1]});
+    v[e] = hv[e] * gg.x;
+    v[e + 1] = hv[e + 1] * gg.y;
+  }
   store8(p, out_row(p, row), ocol, v, true, vec_ok);
 }
 

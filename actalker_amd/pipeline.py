@@ -141,9 +141,10 @@ class HipBackend:
     def max_units_per_call(self) -> int:
         """Largest UNet call (in 14-frame units) whose widest activation stays under the kernels'
         2 GiB buffer extent (32-bit buffer offsets): level-0 rows x 4*C0 bf16 (the GEGLU hidden and
-        the Mamba xz rows). 576x1024, C0 = 320: 91 frames -> 6 units."""
+        the Mamba xz rows; the Mamba sequence adds 33 condition tokens per frame, counted here
+        with margin as 64). 576x1024, C0 = 320: 90 frames -> 6 units."""
         c0 = int(self.unet.config.block_out_channels[0])
-        per_unit = self.F * self.S * 4 * c0 * 2
+        per_unit = self.F * (self.S + 64) * 4 * c0 * 2
         return max(1, (2 ** 31 - 1) // per_unit)
 
     def branch_twins(self) -> dict:

@@ -280,3 +280,15 @@ def test_auto_units_per_call_uses_backend_limit():
     assert sizes == [4, 4, 4] * steps          # 12 units per step, at most 5 per call -> 4 + 4 + 4
     want = oracle_loop(latents, imgl, N, fpb, 1, steps)
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-3)
+
+
+def test_max_units_per_call_stays_under_buffer_extent():
+    """HipBackend.max_units_per_call: widest level-0 activation (rows incl. 33 Mamba condition
+    tokens per frame) x 4*C0 bf16 below 2 GiB; 576x1024 -> 6 units, 576x576 -> 11."""
+    from types import SimpleNamespace
+    for (h, w), want in (((72, 128), 6), ((72, 72), 11)):
+        fake = SimpleNamespace(unet=SimpleNamespace(config=SimpleNamespace(block_out_channels=(320, 640, 1280, 1280))),
+                               F=14, S=h * w)
+        u = pl.HipBackend.max_units_per_call(fake)
+        assert u == want
+        assert u * 14 * (h * w + 33) * 4 * 320 * 2 < 2 ** 31

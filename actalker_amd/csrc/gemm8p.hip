@@ -395,10 +395,22 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       const int row0 = tile_m + qm * 128 + wr * SR;
       const int lc0 = qn * (BN_ / 2) + wc * SC;
       const int col0 = tile_n + lc0;
+      // the residual chunk is loaded one chunk ahead (software pipelined across iterations), so its
+      // HBM latency overlaps the previous chunk's math and store instead of stalling it
+      uint4 rnext = make_uint4(0, 0, 0, 0);
+      auto pre = [&](int chx) {
+        const int rx = chx / CPR, cx = (chx - rx * CPR) * 8;
+        rnext = epi_load_r(p, row0 + rx, col0 + cx, vec_ok && row0 + rx < p.M);
+      };
+      if (p.R) pre(lane);
 #pragma unroll 1
       for (int ch = lane; ch < SR * CPR; ch += 64) {
         const int r = ch / CPR, c8 = (ch - r * CPR) * 8;
         const int row = row0 + r, ocol = col0 + c8;
+        EpiPre e;
+        e.r = rnext;
+        if (p.R && ch + 64 < SR * CPR) pre(ch + 64);
+        if (p.MIX) e.mix = epi_load_mix(p, row, ocol, vec_ok && row < p.M);
         if (row < p.M && ocol < p.N) {
           float v[8];
           const float4 x0 = *reinterpret_cast<const float4*>(&et[r * EPI_LD + c8]);
@@ -419,8 +431,6 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
               add8(v, rb2, ocol + 8 <= p.N && !((size_t)rb2 & 15), p.N - ocol);
             }
           }
-          EpiPre e;
-          epi_prefetch(p, row, ocol, vec_ok, e);
           epilogue8_tail(p, row, ocol, v, vec_ok, e);
         }
       }

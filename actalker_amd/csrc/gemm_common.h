@@ -132,11 +132,21 @@ __device__ __forceinline__ size_t residual_row(const ActhGemmDesc& p, int row) {
 // 16-byte residual / mix chunks of (row, [ocol, ocol+8)) for the vector path. The loads are
 // unconditional per lane (an invalid or partial chunk reads row 0 / column 0 instead and is never
 // used), so the prefetched registers do not live across divergent branches.
-__device__ __forceinline__ void epi_prefetch(const ActhGemmDesc& p, int row, int ocol, bool ok, EpiPre& e) {
+__device__ __forceinline__ uint4 epi_load_r(const ActhGemmDesc& p, int row, int ocol, bool ok) {
   const bool use = ok && ocol + 8 <= p.N;
   const int rr = use ? row : 0, cc = use ? ocol : 0;
-  if (p.R) e.r = *reinterpret_cast<const uint4*>((const bf16_t*)p.R + residual_row(p, rr) * p.ldr + cc);
-  if (p.MIX) e.mix = *reinterpret_cast<const uint4*>((const bf16_t*)p.MIX + (size_t)rr * p.ldmix + cc);
+  return *reinterpret_cast<const uint4*>((const bf16_t*)p.R + residual_row(p, rr) * p.ldr + cc);
+}
+
+__device__ __forceinline__ uint4 epi_load_mix(const ActhGemmDesc& p, int row, int ocol, bool ok) {
+  const bool use = ok && ocol + 8 <= p.N;
+  const int rr = use ? row : 0, cc = use ? ocol : 0;
+  return *reinterpret_cast<const uint4*>((const bf16_t*)p.MIX + (size_t)rr * p.ldmix + cc);
+}
+
+__device__ __forceinline__ void epi_prefetch(const ActhGemmDesc& p, int row, int ocol, bool ok, EpiPre& e) {
+  if (p.R) e.r = epi_load_r(p, row, ocol, ok);
+  if (p.MIX) e.mix = epi_load_mix(p, row, ocol, ok);
 }
 
 // Epilogue after alpha / bias / row bias: residual, SiLU / GELU, AlphaBlender mix, store. The

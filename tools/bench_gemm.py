@@ -24,7 +24,7 @@ SHAPES = [
 ]
 
 
-def run(mode, M, N, K, act, tile, iters, dev, sink=False):
+def run(mode, M, N, K, act, tile, iters, dev, sink=False, residual=False):
     g = torch.Generator(device="cpu").manual_seed(0)
     kw = {}
     if mode == "conv":
@@ -41,6 +41,8 @@ def run(mode, M, N, K, act, tile, iters, dev, sink=False):
         a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)
     bias = torch.randn(N, generator=g).to(dev)
+    if residual and act != 2:   # residual-stream epilogue (attention / proj_out GEMMs)
+        kw["residual"] = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
     if sink:   # every row block writes the same 256 output rows (L2-resident): no HBM write traffic
         kw["out"] = torch.empty(256, N // 2 if act == 2 else N, device=dev, dtype=torch.bfloat16)
         kw["orow"] = (256, 0, 0)
@@ -84,6 +86,7 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated SHAPES indices")
     ap.add_argument("--lib", action="store_true", help="add a torch.matmul (hipBLASLt) column for dense shapes")
     ap.add_argument("--sink", action="store_true", help="write all output row blocks to one 256-row buffer")
+    ap.add_argument("--residual", action="store_true", help="add a bf16 residual (M, N) in the epilogue")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     tiles = [int(t) for t in args.tiles.split(",")]
@@ -95,7 +98,7 @@ def main():
             continue
         cells = []
         for t in tiles:
-            tf, ms = run(mode, M, N, K, act, t | args.flags, args.iters, dev, args.sink)
+            tf, ms = run(mode, M, N, K, act, t | args.flags, args.iters, dev, args.sink, args.residual)
             cells.append(f"{tf:12.1f}" if tf is not None else f"{'n/a':>12s}")
         if args.lib:
             cells.append(f"{run_lib(M, N, K, args.iters, dev):12.1f}" if mode == "dense" else f"{'-':>12s}")

@@ -47,8 +47,14 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
          residual: Optional[torch.Tensor] = None, rmap: Optional[torch.Tensor] = None, r_div: int = 1,
          r_mod: int = 1, mix: Optional[torch.Tensor] = None, mix_alpha: float = 0.0, alpha: float = 1.0,
          act: int = ACT_NONE, out: Optional[torch.Tensor] = None, out_f32: bool = False,
-         orow: Optional[Sequence[int]] = None, tile: int = 0) -> torch.Tensor:
-    """out = epilogue(A . w^T).  ``tile``: 0 auto, 1 128x128, 2 256x256, 3 256x160 (tests force one).  ``w``: packed (N, K) bf16.
+         orow: Optional[Sequence[int]] = None, tile: int = 0, rmap_max: Optional[int] = None) -> torch.Tensor:
+    """out = epilogue(A . w^T).  ``tile``: 0 auto, 1 128x128, 2 256x256, 3 256x160, 4 256x256 8-phase,
+    5 256x320 8-phase (tests force one).  ``w``: packed (N, K) bf16.
+
+    Every operand the kernel reads or writes through a flat pointer is bounds-checked here on the
+    host (the kernels do not check): residual / mix / row-bias rows against M, ``rmap`` entries
+    against ``rmap_max`` (the caller's host-side bound on the map's values), the ``orow`` remap
+    against ``out``.
 
     A modes: dense (a is (M, K1) [+ a2 (M, K-K1)]), ``conv=dict(H, W, Ho, Wo, stride, upsample, B)``
     (a is the NHWC image as (B*H*W, C1) [+ a2]), ``temporal=dict(F, S)`` (a is (M, C1) rows).
@@ -76,6 +82,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
         if K != 9 * cin:
             raise _lib.ActhError(f"conv gemm: weight K={K} != 9*Cin={9 * cin}")
         M = conv["B"] * conv["Ho"] * conv["Wo"]
+        if a.shape[0] < conv["B"] * conv["H"] * conv["W"]:
+            raise _lib.ActhError(f"conv gemm: image has {a.shape[0]} rows < B*H*W")
         d.K1 = c1
     elif temporal is not None:
         cin = c1 + (a2.shape[1] if a2 is not None else 0)
@@ -89,35 +97,54 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
     else:
         d.amode = 0
         M = a.shape[0] if M is None else M
+        if a.shape[0] < M or (a2 is not None and a2.shape[0] < M):
+            raise _lib.ActhError(f"gemm: A has fewer than M={M} rows")
         if a2 is None and a.shape[1] < K:
             raise _lib.ActhError(f"gemm: A has {a.shape[1]} columns < K={K}")
     d.B = w.data_ptr()
     d.ldb = _rows(w, "gemm weight")
     d.M, d.N, d.K = M, N, K
+    n_out = N // 2 if act == ACT_GEGLU else N
     if bias is not None:
         _need(bias, torch.float32, "gemm bias")
+        if bias.numel() < N:
+            raise _lib.ActhError(f"gemm: bias has {bias.numel()} entries < N={N}")
         d.bias = bias.data_ptr()
     if rowbias is not None:
         _need(rowbias, torch.float32, "gemm rowbias")
+        if rb_div < 1 or rowbias.shape[0] < -(-M // rb_div) or rowbias.shape[1] < N:
+            raise _lib.ActhError(f"gemm: rowbias {tuple(rowbias.shape)} too small for ceil(M/{rb_div}) x N={N}")
         d.rowbias = rowbias.data_ptr()
         d.rb_div = rb_div
         d.ldrb = _rows(rowbias, "gemm rowbias")
     if residual is not None:
         _need(residual, torch.bfloat16, "gemm residual")
+        if residual.dim() != 2 or residual.shape[1] < n_out:
+            raise _lib.ActhError(f"gemm: residual {tuple(residual.shape)} narrower than N={n_out}")
         d.R = residual.data_ptr()
         d.ldr = _rows(residual, "gemm residual")
         if rmap is not None:
             _need(rmap, torch.int32, "gemm rmap")
+            if rmap_max is None:
+                raise _lib.ActhError("gemm: rmap needs rmap_max, a host-side bound on its entries")
+            if r_div < 1 or r_mod < 1 or rmap.numel() < min(r_mod, -(-M // r_div)):
+                raise _lib.ActhError(f"gemm: rmap has {rmap.numel()} entries, r_div={r_div} r_mod={r_mod}, M={M}")
+            if (int(rmap_max) + 1) * r_div > residual.shape[0]:
+                raise _lib.ActhError(f"gemm: rmap entries up to {rmap_max} read residual rows beyond "
+                                     f"{residual.shape[0]}")
             d.rmap = rmap.data_ptr()
             d.r_div, d.r_mod = r_div, r_mod
+        elif residual.shape[0] < M:
+            raise _lib.ActhError(f"gemm: residual has {residual.shape[0]} rows < M={M}")
     if mix is not None:
         _need(mix, torch.bfloat16, "gemm mix")
+        if mix.dim() != 2 or mix.shape[0] < M or mix.shape[1] < n_out:
+            raise _lib.ActhError(f"gemm: mix {tuple(mix.shape)} too small for ({M}, {n_out})")
         d.MIX = mix.data_ptr()
         d.ldmix = _rows(mix, "gemm mix")
         d.mix_alpha = float(mix_alpha)
     d.alpha = float(alpha)
     d.act = act
-    n_out = N // 2 if act == ACT_GEGLU else N
     if out is None:
         if orow is not None:
             raise _lib.ActhError("gemm: orow remap needs an explicit output tensor")
@@ -132,7 +159,13 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
         if out.shape[0] < M or out.shape[1] < n_out:
             raise _lib.ActhError(f"gemm: out {tuple(out.shape)} too small for ({M}, {n_out})")
     else:
-        d.orow_div, d.orow_stride, d.orow_off = orow
+        od, ost, oo = (int(v) for v in orow)
+        if od < 1 or ost < 0 or oo < 0:
+            raise _lib.ActhError(f"gemm: bad orow {tuple(orow)}")
+        last = ((M - 1) // od) * ost + (M - 1) % od + oo if M > 0 else -1
+        if out.shape[0] <= last or out.shape[1] < n_out:
+            raise _lib.ActhError(f"gemm: out {tuple(out.shape)} too small for orow {tuple(orow)} at M={M}")
+        d.orow_div, d.orow_stride, d.orow_off = od, ost, oo
     d.tile = tile
     _lib.check(lib.acth_gemm(ctypes.byref(d), _stream()), "acth_gemm")
     return out

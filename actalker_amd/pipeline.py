@@ -192,12 +192,13 @@ class HipBackend:
         ehs = (self.ide[bl, fl], [self.aud[bl, fl], self.vas[bl, fl]])
         cak = {"ip_adapter_masks": self.masks, "acth_gate": self.gate}
         tt = torch.full((1,), t, device=self.dev, dtype=torch.float32)
-        prmap = fidx_d
+        prmap, pmax = fidx_d, int(fidx.max())
         if self.pose_P != self.T:
-            prmap = torch.tensor([r % self.pose_P for (w, _c) in units for r in self._raw[w]],
-                                 dtype=torch.int32).to(self.dev, non_blocking=True)
+            pr = torch.tensor([r % self.pose_P for (w, _c) in units for r in self._raw[w]], dtype=torch.int32)
+            prmap, pmax = pr.to(self.dev, non_blocking=True), int(pr.max())
         noise = self.unet.forward_tokens(x, U, F, self.H, self.W, tt, ehs, self.added[br_d], self.pose, cak,
-                                         spatial_condition_rmap=prmap, out_f32=True)
+                                         spatial_condition_rmap=prmap, out_f32=True,
+                                         spatial_condition_rmap_max=pmax)
         out[row0:row0 + U * F * S].copy_(noise)
 
     def step_windows(self, lat, gathered, unit_rows: List[List[int]], frames, guidance, sigma, sigma_next):
@@ -218,6 +219,21 @@ class HipBackend:
 
 
 # ------------------------------------------------------------------------------------------ loop
+def broadcast_from_rank0(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place broadcast of ``t`` from rank 0 of ``group``. RCCL ("nccl") needs device tensors,
+    gloo host tensors: the tensor is staged through the backend's device when it lives elsewhere."""
+    import torch.distributed as dist
+    on_gpu = dist.get_backend(group) == "nccl"
+    if t.is_cuda == on_gpu:
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        return t
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    tmp = t.to(dev)
+    dist.broadcast(tmp, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    t.copy_(tmp)
+    return t
+
+
 @dataclass
 class LoopConfig:
     num_frames: int
@@ -254,6 +270,11 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
     F = cfg.frames_per_batch
     sigmas, timesteps = karras_sigmas(cfg.num_inference_steps, cfg.sigma_min, cfg.sigma_max)
     lat = backend.new_state(latents_all)
+    if world > 1:
+        # guidance / Euler / accumulation are replicated on every rank with no second collective, so
+        # the latent state must start bitwise identical everywhere: rank 0's copy wins (a caller that
+        # drew its noise from an unseeded per-rank RNG would otherwise run incoherent ranks)
+        broadcast_from_rank0(lat, group)
     n_windows = len(range(0, T, F - cfg.overlap))
     twins = backend.branch_twins() if (cfg.dedup_branches and hasattr(backend, "branch_twins")) else {}
     branches = [c for c in range(4) if c not in twins]

@@ -19,7 +19,7 @@ from typing import List, Optional, Sequence, Union
 
 import torch
 
-from .pipeline import HipBackend, LoopConfig, denoise, karras_sigmas
+from .pipeline import HipBackend, LoopConfig, broadcast_from_rank0, denoise, karras_sigmas
 from .vae import decode_latents
 
 
@@ -113,11 +113,19 @@ class Pose2VideoLongSVDPipeline:
         sigmas, _ = karras_sigmas(num_inference_steps)
         ref = ref_image.to(device).float()
         ref_latents = self.vae.encode(ref).latent_dist.mean * 0.18215
-        aug = torch.randn(ref.shape, generator=generator).to(device)
+        aug = torch.randn(ref.shape, generator=generator)
+        noise = latents if latents is not None else torch.randn((1, T, 4, h, w), generator=generator)
+        if world > 1:
+            # every rank must condition on the same noise-augmented image and start from the same
+            # latents (the loop replicates guidance / Euler per rank): rank 0's draws are broadcast, so an
+            # unseeded per-rank RNG (generator=None under torchrun) cannot make the ranks diverge
+            aug, noise = aug.contiguous(), noise.float().clone()
+            broadcast_from_rank0(aug, group)
+            broadcast_from_rank0(noise, group)
+        aug = aug.to(device)
         image_latents = self._encode_vae_image(ref + noise_aug_strength * aug, device)
         image_latents = image_latents.unsqueeze(1).repeat(1, T, 1, 1, 1)
 
-        noise = latents if latents is not None else torch.randn((1, T, 4, h, w), generator=generator)
         lat0 = ref_latents.unsqueeze(1) + noise.to(device).float() * sigmas[0]          # scheduler.add_noise at t0
 
         pose = torch.stack([p.to(device).float() for p in pose_images], 1)[None] if isinstance(pose_images, list) \

@@ -308,8 +308,11 @@ class UNetSpatioTemporalConditionModel(nn.Module):
     def forward_tokens(self, x_tok: torch.Tensor, B: int, F: int, H: int, W: int, timestep, encoder_hidden_states,
                        added_time_ids, spatial_condition_tok: Optional[torch.Tensor] = None,
                        cross_attention_kwargs: Optional[Dict[str, Any]] = None,
-                       spatial_condition_rmap: Optional[torch.Tensor] = None, out_f32: bool = True):
-        """Token-major entry: x_tok (B*F*H*W, in_channels) bf16 -> (B*F*H*W, out_channels)."""
+                       spatial_condition_rmap: Optional[torch.Tensor] = None, out_f32: bool = True,
+                       spatial_condition_rmap_max: Optional[int] = None):
+        """Token-major entry: x_tok (B*F*H*W, in_channels) bf16 -> (B*F*H*W, out_channels).
+        ``spatial_condition_rmap`` (device int32, one entry per frame) remaps frame rows of
+        ``spatial_condition_tok``; ``spatial_condition_rmap_max`` is the host-side bound on its entries."""
         if self.device.type != "cuda":
             raise RuntimeError("UNetSpatioTemporalConditionModel (actalker_amd) runs on the MI355X HIP kernels "
                                "only; move it to a GPU device first")
@@ -323,7 +326,10 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             kw = dict(residual=spatial_condition_tok)
             if spatial_condition_rmap is not None:
                 # row (u*F + f)*S0 + s reads spatial_condition row rmap[u*F + f]*S0 + s
-                kw.update(rmap=spatial_condition_rmap, r_div=S0, r_mod=spatial_condition_rmap.numel())
+                if spatial_condition_rmap_max is None:
+                    raise ValueError("spatial_condition_rmap needs spatial_condition_rmap_max")
+                kw.update(rmap=spatial_condition_rmap, r_div=S0, r_mod=spatial_condition_rmap.numel(),
+                          rmap_max=spatial_condition_rmap_max)
         h = ops.gemm(cols, self._conv_in_w(), bias=self.conv_in.b(), **kw)
         del cols
         skips = [h]

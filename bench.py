@@ -186,28 +186,41 @@ class GemmTimer:
 def cpu_baseline(unet, H, W, frames=2, mode=0):
     """Oracle (fp32 CPU restatement) on a bounded sample: one UNet call, 1 CFG branch x `frames`
     frames at full resolution; frames/s extrapolated to the N=14 workload (200 frame-forwards
-    per output frame = 4 CFG x 25 steps x 28/14)."""
+    per output frame = 4 CFG x 25 steps x 28/14). The HIP UNet runs the same call on the same
+    weights and inputs, and the two outputs are compared (the bench line's ``parity``)."""
     from oracle import reference_cpu as ref
     sd = {k: v.detach().float().cpu() for k, v in unet.state_dict().items()}
     g = torch.Generator().manual_seed(1)
     h, w = H // 8, W // 8
     sample = torch.randn(1, frames, 8, h, w, generator=g)
-    ehs = (torch.randn(frames, 1, 1024, generator=g),
-           [torch.randn(frames, 32, 1024, generator=g), torch.randn(frames, 1, 1024, generator=g) * (mode != 0)])
+    aud = torch.randn(frames, 32, 1024, generator=g) * float(mode != 1)       # gate (pipeline:724)
+    vas = torch.randn(frames, 1, 1024, generator=g) * float(mode != 0)
+    ehs = (torch.randn(frames, 1, 1024, generator=g), [aud, vas])
     pose = 0.1 * torch.randn(1, frames, 320, h, w, generator=g)
-    masks = [torch.ones(1, 1, H, W), torch.ones(1, 1, H, W) if mode != 0 else torch.zeros(1, 1, H, W)]
-    if mode == 1:
-        masks = [torch.zeros(1, 1, H, W), torch.ones(1, 1, H, W)]
+    one, zero = torch.ones(1, 1, H, W), torch.zeros(1, 1, H, W)
+    masks = {0: [one, zero], 1: [zero, one], 2: [one, one]}[mode]             # pipeline:702-711
+    t = torch.tensor(1.6)
+    added = torch.tensor([[12.5, 12.0, 20.0]])
     t0 = time.perf_counter()
     with torch.no_grad():
-        ref.unet_forward(sd, sample, torch.tensor(1.6), ehs, torch.tensor([[12.5, 12.0, 20.0]]), pose,
-                         {"ip_adapter_masks": masks})
+        want = ref.unet_forward(sd, sample, t, ehs, added, pose, {"ip_adapter_masks": masks})
     dt = time.perf_counter() - t0
+    dev = unet.device
+    with torch.no_grad():
+        got = unet(sample.to(dev), t.to(dev), (ehs[0].to(dev), [e.to(dev) for e in ehs[1]]), added.to(dev),
+                   spatial_condition=pose.to(dev), cross_attention_kwargs={"ip_adapter_masks": masks},
+                   return_dict=False)[0].float().cpu()
+    d = got - want
+    parity = dict(rel_l2=round((d.norm() / want.norm()).item(), 6), max_abs=round(d.abs().max().item(), 5),
+                  ref_rms=round(want.pow(2).mean().sqrt().item(), 5), tol_rel_l2=2e-2,
+                  sample=f"HIP bf16 vs oracle fp32, one UNet call (1 CFG branch x {frames} frames, {H}x{W}, "
+                         f"mode {mode} masks / gated prompts), same weights and inputs")
     per_frame_fwd = dt / frames
     fps = 1.0 / (per_frame_fwd * 200.0)
-    return dict(value=fps, unit="frames/s", cores=torch.get_num_threads(), kind="port",
+    base = dict(value=fps, unit="frames/s", cores=torch.get_num_threads(), kind="port",
                 sample=f"oracle fp32 UNet call, 1 CFG branch x {frames} frames at {H}x{W} ({dt:.1f} s = "
                        f"{per_frame_fwd:.2f} s/frame-forward), extrapolated x200 frame-forwards per output frame")
+    return base, parity
 
 
 def main():
@@ -310,9 +323,9 @@ def main():
                     kernel_share_of_step=round(gemm_ms / (elapsed * 1000.0), 3))
     n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank, branches=branches)[0])
     frame_fwds = n_units_rank * fpb * args.steps
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(unet_cpu, H, W, frames=args.cpu_frames, mode=args.mode)
+        cpu, parity = cpu_baseline(unet, H, W, frames=args.cpu_frames, mode=args.mode)
     if rank == 0:
         line = {
             "metric": "denoised frames/sec, 576x1024x14f x25-step audio-driven, 1/2/4/8 MI355X",
@@ -332,6 +345,7 @@ def main():
             "finite": ok,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

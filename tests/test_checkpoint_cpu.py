@@ -125,3 +125,25 @@ def test_vae_from_pretrained_folder(tmp_path):
     v = AutoencoderKLTemporalDecoder.from_pretrained(str(tmp_path), subfolder="vae", variant="fp16")
     assert v.config.block_out_channels == (64, 64, 128, 128)
     assert torch.equal(v.state_dict()["quant_conv.weight"], sd["quant_conv.weight"].half().float())
+
+
+def test_unet_state_dict_layout_matches_reference():
+    """Every key and shape of the reference UNet (default SVD-XT config, after the reference
+    add_ip_adapters(unet, [32, 32], [1.25, 1.25]); tools/gen_golden_keys.py imports the reference
+    package by path) equals this build's, so a real ACTalker checkpoint loads with strict=True
+    (Inference.py:124-127); the config fields match too (v10:73-99)."""
+    import json
+    from actalker_amd.unet_spatio_temporal_condition_mambaID_v10_two_ip import (UNetSpatioTemporalConditionModel,
+                                                                               add_ip_adapters)
+    with open(os.path.join(os.path.dirname(__file__), "golden", "unet_reference_keys.json")) as fh:
+        ref_layout = json.load(fh)
+    with torch.device("meta"):
+        unet = UNetSpatioTemporalConditionModel()
+    add_ip_adapters(unet, [32, 32], [1.25, 1.25])
+    ours = {k: list(v.shape) for k, v in unet.state_dict().items()}
+    want = ref_layout["keys"]
+    assert sorted(set(want) - set(ours)) == [] and sorted(set(ours) - set(want)) == []
+    assert {k: v for k, v in ours.items() if want[k] != v} == {}
+    for k, v in ref_layout["config"].items():
+        got = getattr(unet.config, k)
+        assert (list(got) if isinstance(got, tuple) else got) == v, k

@@ -1,0 +1,157 @@
+"""GPU parity at the BASELINE geometry and over the full 25-step schedule.
+
+* UNet forward at 576x1024 (latent 72x128), real widths 320/640/1280/1280 and heads 5/10/20/20,
+  B = 1 CFG branch x F = 2 frames, four mask cases (modes 0 / 1 / 2 and half masks), against the fp32
+  oracle's output on the same seeded weights and inputs (tests/golden/unet_full_*.safetensors,
+  tools/gen_golden_full.py). This is the shape the reference's UNet call runs (v10:362-517) with
+  S0 = 9216 spatial attention and Mamba scans of length 9249 / 2337 / 609 (mamba_layer.py:1532).
+  Tolerance (bf16 activations, fp32 accumulation vs fp32 CPU): relative L2 <= 2e-2 and max |err| <=
+  0.25 on an output of rms ~1 (measured values are printed and, with ACTH_PARITY_LOG set, appended
+  to that file as JSON lines).
+* The selective scan at the level shapes (L = 9249 / 9218 / 2337 / 609, D = 640 / 1280 / 2560) and
+  flash attention at S = 9216 (5 heads) and 2304 (10 heads) against the oracle's restatements.
+* The sampler loop over all 25 Karras steps (sigma 700 -> 0.002) for modes 0 / 1 / 2 against the
+  oracle loop's final latents (tests/golden/loop25_*.safetensors, tools/gen_golden_loop.py).
+"""
+import json
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+from safetensors.torch import load_file
+
+from oracle import reference_cpu as ref
+from tests import golden_full as gf
+from tests import golden_loop as gl
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _stats(got, want):
+    got = got.float().cpu()
+    want = want.float().cpu()
+    d = got - want
+    return dict(rel_l2=(d.norm() / want.norm()).item(), max_abs=d.abs().max().item(),
+                ref_rms=want.pow(2).mean().sqrt().item())
+
+
+def _log(name, st):
+    print(name, json.dumps(st))
+    path = os.environ.get("ACTH_PARITY_LOG")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps(dict(test=name, **st)) + "\n")
+
+
+# ------------------------------------------------------------------------------------------ UNet
+@pytest.fixture(scope="module")
+def full_unet(dev):
+    unet = gf.build_full_unet()
+    sd = unet.state_dict()
+    wsum = gf.checksum(*[sd[k] for k in sorted(sd)])
+    return unet.to(dev), wsum
+
+
+@pytest.mark.parametrize("case", gf.CASES)
+def test_unet_full_geometry_matches_oracle(dev, full_unet, case):
+    unet, wsum = full_unet
+    g = load_file(os.path.join(GOLD, f"unet_full_{case}.safetensors"))
+    # fp64 sums over 1.8 B values: the reduction order (thread count) moves the last digits only
+    torch.testing.assert_close(wsum, g["weights_checksum"], rtol=1e-6, atol=1e-6)
+    sample, t, ehs, added, pose, masks = gf.case_inputs(case)
+    torch.testing.assert_close(gf.checksum(sample, ehs[0], *ehs[1], pose, *masks), g["inputs_checksum"],
+                               rtol=1e-6, atol=1e-6)
+    out = unet(sample.to(dev), t.to(dev), (ehs[0].to(dev), [e.to(dev) for e in ehs[1]]), added.to(dev),
+               spatial_condition=pose.to(dev), cross_attention_kwargs={"ip_adapter_masks": masks},
+               return_dict=False)[0]
+    st = _stats(out, g["out"])
+    _log(f"unet_full_{case}", st)
+    assert torch.isfinite(out).all()
+    assert st["rel_l2"] < 2e-2, st
+    assert st["max_abs"] < 0.25 * max(1.0, st["ref_rms"]), st
+
+
+# ------------------------------------------------------------------------------------------ scan
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("S,C,n_cond", [(9216, 320, 33), (9216, 320, 2), (2304, 640, 33), (576, 1280, 33)])
+def test_selective_scan_level_shapes(dev, S, C, n_cond):
+    """One batch element of a level's scan: L = S + n_cond (audio branch 33 = ID + 32 audio tokens,
+    expression branch 2 = ID + 1 VASA token), D = d_inner = 2C, R = ceil(C / 16), outputs kept for
+    the S image tokens (mamba_layer.py:1965-1969, 1505-1548)."""
+    from actalker_amd import ops
+    g = torch.Generator().manual_seed(S + n_cond)
+    D, R, L = 2 * C, -(-C // 16), S + n_cond
+    u = _bf(torch.randn(L, D, generator=g))
+    xproj = torch.randn(2 * (R + 32), D, generator=g) * D ** -0.5
+    dtw = (torch.rand(2, D, R, generator=g) * 2 - 1) * R ** -0.5
+    dt = torch.exp(torch.rand(2, D, generator=g) * (torch.log(torch.tensor(0.1)) - torch.log(torch.tensor(0.001)))
+                   + torch.log(torch.tensor(0.001)))
+    dtb = dt + torch.log(-torch.expm1(-dt))
+    alog = torch.log(torch.arange(1, 17).float()).repeat(2 * D, 1) + 0.1 * torch.randn(2 * D, 16, generator=g)
+    Dp = 1 + 0.1 * torch.randn(2 * D, generator=g)
+    xdbl = u.float() @ _bf(xproj).float().t()
+    y0, y1 = ops.selective_scan(u.to(dev), xdbl.to(dev), dtw.to(dev), dtb.to(dev), alog.to(dev), Dp.to(dev),
+                                nb=1, L=L, R=R, n_keep=S)
+    W = R + 32
+    x = u.float().t()[None]                                        # (1, D, L)
+    xs = torch.stack([x, torch.flip(x, dims=[-1])], 1)
+    x_dbl = torch.einsum("b k d l, k c d -> b k c l", xs, _bf(xproj).float().view(2, W, D))
+    dts, Bs, Cs = torch.split(x_dbl, [R, 16, 16], dim=2)
+    dts = torch.einsum("b k r l, k d r -> b k d l", dts, dtw)
+    out = ref.selective_scan_ref(xs.reshape(1, 2 * D, L), dts.reshape(1, 2 * D, L), -torch.exp(alog), Bs, Cs, Dp,
+                                 delta_bias=dtb.reshape(-1), delta_softplus=True).view(1, 2, D, L)
+    r0 = out[0, 0, :, :S].t()
+    r1 = torch.flip(out[0, 1], dims=[-1])[:, :S].t()
+    s0, s1 = _stats(y0, r0), _stats(y1, r1)
+    _log(f"scan_L{L}_D{D}", dict(dir0=s0, dir1=s1))
+    assert s0["rel_l2"] < 1e-2 and s1["rel_l2"] < 1e-2, (s0, s1)
+
+
+@pytest.mark.parametrize("S,heads", [(9216, 5), (2304, 10)])
+def test_flash_attn_level_shapes(dev, S, heads):
+    from actalker_amd import ops
+    g = torch.Generator().manual_seed(S)
+    C = heads * 64
+    qkv = _bf(torch.randn(S, 3 * C, generator=g))
+    out = ops.flash_attn(qkv.to(dev), 1, S, heads)
+    q, k, v = qkv.float().view(1, S, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    refo = F.scaled_dot_product_attention(q, k, v).permute(0, 2, 1, 3).reshape(S, C)
+    st = _stats(out, refo)
+    _log(f"flash_S{S}_H{heads}", st)
+    assert st["rel_l2"] < 1e-2, st
+
+
+# ------------------------------------------------------------------------------------------ loop
+@pytest.fixture(scope="module")
+def loop_unet(dev):
+    import __graft_entry__ as ge
+    unet, cfg = ge._tiny_unet(seed=gl.UNET_SEED)
+    return unet.to(dev)
+
+
+@pytest.mark.parametrize("mode", sorted(gl.GATES))
+def test_pipeline_25_steps_matches_oracle(dev, loop_unet, mode):
+    """All 25 Karras steps (sigma 700 -> 0.002) of the windowed 4-way-CFG loop, dedup on (modes 0 / 1
+    evaluate 3 branches), vs the oracle loop's final latents. Tolerance: relative L2 <= 3e-2 on the
+    final latents (bf16 UNet, fp32 latent state)."""
+    from actalker_amd import pipeline as pl
+    latents, imgl, ide, aud, vas, pose, added, masks = gl.loop_inputs()
+    gate = gl.GATES[mode]
+    T = gl.N + gl.FPB
+    backend = pl.HipBackend(loop_unet, gl.H, gl.W, masks, gate, added, T, gl.FPB, imgl, ide, aud, vas, pose)
+    twins = backend.branch_twins()
+    assert twins == {"mode0": {3: 2}, "mode1": {2: 1}, "mode2": {}}[mode]
+    lc = pl.LoopConfig(num_frames=gl.N, frames_per_batch=gl.FPB, overlap=0, shift_offset=gl.SHIFT,
+                       num_inference_steps=25)
+    with torch.no_grad():
+        got = pl.denoise(backend, latents, lc)
+    want = load_file(os.path.join(GOLD, f"loop25_{mode}.safetensors"))["latents"]
+    st = _stats(got, want)
+    _log(f"loop25_{mode}", st)
+    assert torch.isfinite(got).all()
+    assert st["rel_l2"] < 3e-2, st

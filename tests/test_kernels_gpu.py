@@ -65,7 +65,7 @@ def test_gemm_epilogues(dev):
     rmap = torch.tensor([2, 0, 1], dtype=torch.int32)
     res3 = bf(rnd(3 * 57, N))
     out = ops.gemm(a.to(dev), w2.to(dev), a2=a2.to(dev), residual=res3.to(dev), rmap=rmap.to(dev), r_div=57,
-                   r_mod=3, M=M)
+                   r_mod=3, M=M, rmap_max=2)
     rows = torch.arange(M)
     rr = rmap[(rows // 57) % 3].long() * 57 + rows % 57
     refo = torch.cat([a, a2], 1).float() @ w2.float().t() + res3.float()[rr]
@@ -112,6 +112,56 @@ def test_gemm_grouped_raster(dev, tile, gm):
         out = ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), tile=tile | (gm << 16))
         assert rel(out, a.float() @ w.float().t() + bias) < 1e-2
         assert torch.equal(out, ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), tile=tile))
+
+
+@pytest.mark.parametrize("tile", [4, 5])
+@pytest.mark.parametrize("case", ["plain", "rmap_mix_silu", "ragged_n"])
+def test_gemm_phased_vector_residual(dev, tile, case):
+    """The phased kernels' vector residual path (16-byte-aligned residual rows, the residual chunk
+    loaded one iteration ahead, invalid rows / columns clamped to row 0): N a multiple of 8, a
+    ragged last row tile, residual through a row map, AlphaBlender mix and SiLU; "ragged_n" adds a
+    partial last 8-column chunk (scalar fallback beside the vector chunks of the same rows)."""
+    M, K = 11 * 256 - 40, 192
+    N = 640 if case != "ragged_n" else 644
+    a, w = bf(rnd(M, K)), bf(rnd(N, K, scale=K ** -0.5))
+    bias = rnd(N)
+    if case == "rmap_mix_silu":
+        r_div = 97
+        nq = -(-M // r_div)
+        rmap = torch.randperm(nq).to(torch.int32)
+        res = bf(rnd(nq * r_div, N))
+        mix = bf(rnd(M, N))
+        out = ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), residual=res.to(dev), rmap=rmap.to(dev), r_div=r_div,
+                       r_mod=nq, rmap_max=nq - 1, act=ops.ACT_SILU, mix=mix.to(dev), mix_alpha=0.3, tile=tile)
+        rows = torch.arange(M)
+        rr = rmap[rows // r_div].long() * r_div + rows % r_div
+        refo = 0.3 * mix.float() + 0.7 * F.silu(a.float() @ w.float().t() + bias + res.float()[rr])
+    else:
+        res = bf(rnd(M, N))
+        out = ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), residual=res.to(dev), tile=tile)
+        refo = a.float() @ w.float().t() + bias + res.float()
+    assert out.shape == (M, N)
+    assert rel(out, refo) < 1e-2
+    # every row, including the ragged last tile, individually
+    err_rows = ((out.float().cpu() - refo).norm(dim=1) / refo.norm(dim=1)).max().item()
+    assert err_rows < 2e-2, err_rows
+
+
+def test_gemm_host_bounds_checks(dev):
+    """ops.gemm refuses operands the kernel would read or write out of bounds."""
+    from actalker_amd._lib import ActhError
+    a, w = bf(rnd(300, 64)).to(dev), bf(rnd(128, 64)).to(dev)
+    with pytest.raises(ActhError):
+        ops.gemm(a, w, residual=bf(rnd(299, 128)).to(dev))
+    with pytest.raises(ActhError):
+        ops.gemm(a, w, mix=bf(rnd(300, 64)).to(dev), mix_alpha=0.5)
+    with pytest.raises(ActhError):
+        ops.gemm(a, w, rowbias=rnd(2, 128).to(dev), rb_div=100)
+    with pytest.raises(ActhError):
+        ops.gemm(a, w, residual=bf(rnd(200, 128)).to(dev), rmap=torch.tensor([0, 1, 2], dtype=torch.int32, device=dev),
+                 r_div=100, r_mod=3, rmap_max=2)
+    with pytest.raises(ActhError):
+        ops.gemm(a, w, out=torch.empty(300, 128, device=dev, dtype=torch.bfloat16), orow=(100, 110, 0))
 
 
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])

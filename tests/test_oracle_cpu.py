@@ -110,3 +110,26 @@ def test_mask_downsample_geometry_and_ones():
     half[:, 288:] = 1.0
     md = ref.mask_downsample(half, 1, 9216, 1)
     assert int(md.view(-1).int().nonzero().numel()) == 4608
+
+
+# ------------------------------------------------------------------------------------------
+# the oracle's attention restatement against the REFERENCE processors' goldens (tools/gen_golden_attn.py)
+@pytest.mark.parametrize("name", ["self_temporal_s576", "ip_temporal_s576", "ip_half_s576_c1280", "ip_half_s9216",
+                                  "ip_zeros_s9216", "self_s9216"])
+def test_oracle_attention_matches_reference_processor_golden(name):
+    from safetensors.torch import load_file
+    from tests import golden_attn as ga
+    case = ga.CASES[name]
+    sd = {"a." + k: v for k, v in ga.weights(name, case).items()}
+    x, ide, aud, vas = ga.inputs(name, case)
+    if case["kind"].startswith("self"):
+        y = ref.attn_processor(sd, "a", x, case["heads"])
+    elif case["kind"] == "ip":
+        y = ref.ip_attn_processor(sd, "a", x, case["heads"], (ide, [aud, vas]), (1.25, 1.25), ga.masks(case["mask"]))
+    else:
+        S = case["S"]
+        rep = lambda t: t.repeat_interleave(S, dim=0)               # noqa: E731
+        y = ref.ip_attn_processor(sd, "a", x, case["heads"], (rep(ide), [rep(aud), rep(vas)]), (1.25, 1.25), None)
+    want = load_file(os.path.join(GOLD, f"attn_{name}.safetensors"))["y"]
+    got = ga.subsample(y, case)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)

@@ -292,3 +292,75 @@ def test_max_units_per_call_stays_under_buffer_extent():
         u = pl.HipBackend.max_units_per_call(fake)
         assert u == want
         assert u * 14 * (h * w + 33) * 4 * 320 * 2 < 2 ** 31
+
+
+# ------------------------------------------------------------------------------------------
+# Pose2VideoLongSVDPipeline on 2 gloo ranks with generator=None: the ranks draw their
+# noise from different global RNG states; rank 0's draws must win everywhere.
+class _Obj:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class _FakeVae:
+    """encode(x) -> latent_dist with mean / mode(): 8x average-pooled first 4 'channels'."""
+
+    def encode(self, x):
+        lat = torch.nn.functional.avg_pool2d(x.float(), 8)
+        lat = torch.cat([lat, lat[:, :1]], 1)[:, :4]
+        return _Obj(latent_dist=_Obj(mean=lat, mode=lambda: lat))
+
+
+class _FakeUnet:
+    device = torch.device("cpu")
+    config = _Obj(addition_time_embed_dim=256)
+    add_embedding = _Obj(linear_1=_Obj(in_features=768))
+
+
+class _SvdCpuBackend(CpuBackend):
+    """pipeline.HipBackend's constructor signature over the CPU stand-in UNet."""
+
+    def __init__(self, unet, H, W, masks, gate, added_time_ids, T, fpb, image_latents, image_embeddings,
+                 audio_prompts, vasa_prompts, pose_fea):
+        super().__init__(image_latents.float(), H, W, T, fpb)
+
+
+def _svd_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from actalker_amd import pipeline_svd as ps
+        ps.HipBackend = _SvdCpuBackend
+        torch.manual_seed(1000 + rank)                       # deliberately different per-rank RNG state
+        N, fpb, H, W = 4, 2, 16, 24
+        pipe = ps.Pose2VideoLongSVDPipeline(vae=_FakeVae(), unet=_FakeUnet(),
+                                            id_proj_model=lambda x: x.float().mean() * torch.ones(1, 1, 1024),
+                                            pose_guider=lambda p: torch.zeros(1, 320, p.shape[2], H // 8, W // 8))
+        ref = torch.linspace(-1, 1, 3 * H * W).view(1, 3, H, W)
+        pose = [torch.ones(3, H, W) for _ in range(N)]
+        masks = [torch.ones(1, H, W) for _ in range(N)]
+        a = [torch.zeros(32, 1024) for _ in range(N)]
+        v = [torch.zeros(1024) for _ in range(N)]
+        out = pipe(ref, torch.zeros(1, 512), pose, masks, masks, a, a, v, v, height=H, width=W, num_frames=N,
+                   num_inference_steps=3, frames_per_batch=fpb, overlap=0, shift_offset=1, output_type="latent",
+                   generator=None, world=world, rank=rank).frames
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_svd_pipeline_ranks_agree_without_generator():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_svd_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])

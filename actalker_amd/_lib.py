@@ -91,6 +91,7 @@ class GroupNormDesc(ctypes.Structure):
         ("silu", c_int),
         ("y", c_vp), ("ldy", c_int),
         ("ws", c_vp),
+        ("res", c_vp), ("ldres", c_int),
     ]
 
 
@@ -141,6 +142,10 @@ SIGNATURES = {
     "acth_temporal_attn": ([_P(TemporalAttnDesc), c_vp], c_int),
     "acth_ip_attn": ([_P(IpAttnDesc), c_vp], c_int),
     "acth_layernorm": ([_P(LayerNormDesc), c_vp], c_int),
+    "acth_im2col": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
+                     c_vp], c_int),
+    "acth_maxpool2d": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
+                        c_vp], c_int),
     "acth_groupnorm": ([_P(GroupNormDesc), c_vp], c_int),
     "acth_groupnorm_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
     "acth_mamba_combine_ln": ([_P(MambaCombineDesc), c_vp], c_int),

@@ -3,7 +3,8 @@
 //  * acth_timestep_embedding : diffusers/TransformerSTmodel get_timestep_embedding
 //                              (TransformerSTmodel.py:43-96), bf16 output
 //  * acth_nchw_to_tokens / acth_tokens_to_nchw : (B, C, H, W) <-> (B*H*W, C) layout change
-//  * acth_im2col3x3          : explicit im2col for convs with Cin % 64 != 0 (conv_in: Cin = 8)
+//  * acth_im2col(3x3)        : explicit im2col for convs with Cin % 64 != 0 (conv_in: Cin = 8, 7x7 stems)
+//  * acth_maxpool2d          : nn.MaxPool2d on NHWC rows (VASA ResNet stems)
 //  * acth_gather_rows        : Mamba token selection xz[:, idx] (mamba_layer.py:1963)
 //  * acth_frame_mean         : spatial2time context pooling, mean over frames
 //                              (TransformerSTmodel.py:4037-4052)
@@ -97,32 +98,85 @@ extern "C" int acth_tokens_to_nchw(const void* x, int in_dt, int ldx, void* y, i
 }
 
 // ------------------------------------------------------------------------------------------
-// im2col for a 3x3 / pad 1 / stride 1 conv on NHWC bf16: out[m, (ky*3+kx)*C + c], ld = Kpad
-// (columns >= 9C are zero-filled).
-__global__ void im2col_kernel(const bf16_t* x, int B, int H, int W, int C, bf16_t* out, int Kpad) {
+// im2col for a kh x kw / stride / pad conv on NHWC bf16 rows (ld ldx): out[m, (ky*kw+kx)*C + c],
+// m = (b*Ho + yo)*Wo + xo, ld = Kpad (columns >= kh*kw*C are zero-filled). Used where Cin is too
+// narrow for the implicit-GEMM loader (UNet conv_in: Cin = 8; VASA ResNet stems: 7x7 / stride 2, Cin = 3).
+__global__ void im2col_kernel(const bf16_t* x, int ldx, int B, int H, int W, int C, int kh, int kw, int stride,
+                              int pad, int Ho, int Wo, bf16_t* out, int Kpad) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long M = (long long)B * H * W;
+  const long long M = (long long)B * Ho * Wo;
   if (idx >= M * Kpad) return;
   const long long m = idx / Kpad;
   const int k = (int)(idx - m * Kpad);
   bf16_t v = 0;
-  if (k < 9 * C) {
+  if (k < kh * kw * C) {
     const int tap = k / C, c = k - tap * C;
-    const int ky = tap / 3, kx = tap - ky * 3;
-    const long long b = m / (H * W);
-    const int rem = (int)(m - b * H * W);
-    const int y = rem / W + ky - 1, xx = rem % W + kx - 1;
-    if (y >= 0 && y < H && xx >= 0 && xx < W) v = x[((b * H + y) * W + xx) * C + c];
+    const int ky = tap / kw, kx = tap - ky * kw;
+    const long long b = m / ((long long)Ho * Wo);
+    const int rem = (int)(m - b * Ho * Wo);
+    const int y = (rem / Wo) * stride + ky - pad, xx = (rem % Wo) * stride + kx - pad;
+    if (y >= 0 && y < H && xx >= 0 && xx < W) v = x[((b * H + y) * W + xx) * ldx + c];
   }
   out[idx] = v;
 }
 
+extern "C" int acth_im2col(const void* x, int ldx, int B, int H, int W, int C, int kh, int kw, int stride, int pad,
+                           int Ho, int Wo, void* out, int Kpad, hipStream_t stream) {
+  if (!x || !out || B <= 0 || C <= 0 || ldx < C || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0) return ACTH_EINVAL;
+  if (Kpad < kh * kw * C || Ho != (H + 2 * pad - kh) / stride + 1 || Wo != (W + 2 * pad - kw) / stride + 1)
+    return ACTH_EINVAL;
+  const long long n = (long long)B * Ho * Wo * Kpad;
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const bf16_t*)x, ldx, B, H, W, C, kh, kw, stride, pad, Ho, Wo, (bf16_t*)out, Kpad);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
 extern "C" int acth_im2col3x3(const void* x, int B, int H, int W, int C, void* out, int Kpad,
                               hipStream_t stream) {
-  if (!x || !out || Kpad < 9 * C || B <= 0) return ACTH_EINVAL;
-  const long long n = (long long)B * H * W * Kpad;
-  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                     (const bf16_t*)x, B, H, W, C, (bf16_t*)out, Kpad);
+  return acth_im2col(x, C, B, H, W, C, 3, 3, 1, 1, H, W, out, Kpad, stream);
+}
+
+// ------------------------------------------------------------------------------------------
+// nn.MaxPool2d(k, stride, pad) on NHWC bf16 rows (padding never wins: PyTorch pads with -inf);
+// one thread per (output pixel, 8-channel chunk), 16-byte loads / stores.
+__global__ void maxpool_kernel(const bf16_t* x, int ldx, int B, int H, int W, int C, int k, int stride, int pad,
+                               int Ho, int Wo, bf16_t* y, int ldy) {
+  const int nch = C >> 3;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)B * Ho * Wo * nch) return;
+  const int ch = (int)(t % nch);
+  const long long m = t / nch;
+  const long long b = m / ((long long)Ho * Wo);
+  const int rem = (int)(m - b * Ho * Wo);
+  const int yo = rem / Wo, xo = rem - yo * Wo;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = -INFINITY;
+  for (int ky = 0; ky < k; ++ky) {
+    const int yi = yo * stride + ky - pad;
+    if (yi < 0 || yi >= H) continue;
+    for (int kx = 0; kx < k; ++kx) {
+      const int xi = xo * stride + kx - pad;
+      if (xi < 0 || xi >= W) continue;
+      float w[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + ((b * H + yi) * W + xi) * ldx + ch * 8), w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], w[e]);
+    }
+  }
+  *reinterpret_cast<uint4*>(y + m * ldy + ch * 8) = pack8(v);
+}
+
+extern "C" int acth_maxpool2d(const void* x, int ldx, int B, int H, int W, int C, int k, int stride, int pad,
+                              int Ho, int Wo, void* y, int ldy, hipStream_t stream) {
+  if (!x || !y || B <= 0 || C % 8 || ldx % 8 || ldy % 8 || k <= 0 || stride <= 0 || pad < 0 || 2 * pad > k)
+    return ACTH_EINVAL;
+  if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1 || Ho <= 0 || Wo <= 0)
+    return ACTH_EINVAL;
+  const long long n = (long long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const bf16_t*)x, ldx, B, H, W, C, k, stride, pad, Ho, Wo, (bf16_t*)y, ldy);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -287,6 +287,27 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p
   }
 }
 
+// y = act(x * a + b [+ res]) for one 8-channel chunk of a row, stored as 16 bytes
+__device__ __forceinline__ void gn_finish(const ActhGroupNormDesc& p, long long row, int ch, float* v, const float* sa,
+                                          const float* sb) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = v[e] * sa[e] + sb[e];
+  if (p.res) {
+    float r[8];
+    unpack8(*reinterpret_cast<const uint4*>((const bf16_t*)p.res + row * p.ldres + ch * 8), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r[e];
+  }
+  if (p.silu == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+  } else if (p.silu == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+  }
+  *reinterpret_cast<uint4*>((bf16_t*)p.y + row * p.ldy + ch * 8) = pack8(v);
+}
+
 // grid: M / rows_per_blk blocks; every block's rows lie in one statistics batch
 __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p, int rows_per_blk) {
   const int nch = p.C >> 3;
@@ -330,23 +351,13 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p
       for (int u = 0; u < 4; ++u) {
         float v[8];
         unpack8(w[u], v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float o = v[e] * sa[k][e] + sb[k][e];
-          v[e] = p.silu ? silu_f(o) : o;
-        }
-        *reinterpret_cast<uint4*>((bf16_t*)p.y + (row0 + r + u * rows_par) * p.ldy + ch * 8) = pack8(v);
+        gn_finish(p, row0 + r + u * rows_par, ch, v, sa[k], sb[k]);
       }
     }
     for (; r < rows_per_blk; r += rows_par) {
       float v[8];
       unpack8(gn_load(p, row0 + r, ch), v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float o = v[e] * sa[k][e] + sb[k][e];
-        v[e] = p.silu ? silu_f(o) : o;
-      }
-      *reinterpret_cast<uint4*>((bf16_t*)p.y + (row0 + r) * p.ldy + ch * 8) = pack8(v);
+      gn_finish(p, row0 + r, ch, v, sa[k], sb[k]);
     }
   }
 }
@@ -362,7 +373,8 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   if (d->C % 8 || d->C1 % 8 || d->G <= 0 || d->C % d->G || d->rows_per_stat <= 0) return ACTH_EINVAL;
   if (d->M % d->rows_per_stat) return ACTH_EINVAL;
   if (d->C1 < d->C && (!d->x2 || d->ldx2 % 8)) return ACTH_EINVAL;
-  if (d->ldx % 8 || d->ldy % 8 || d->C > 4096) return ACTH_EINVAL;
+  if (d->ldx % 8 || d->ldy % 8 || d->C > 4096 || d->silu < 0 || d->silu > 2) return ACTH_EINVAL;
+  if (d->res && d->ldres % 8) return ACTH_EINVAL;
   const int nstat = d->M / d->rows_per_stat;
   if (nstat == 0) return ACTH_OK;
   if (nstat > 65535) return ACTH_EINVAL;

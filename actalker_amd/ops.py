@@ -265,7 +265,8 @@ def layernorm(x: torch.Tensor, gamma, beta, eps: float = 1e-5, *, add=None, add_
 
 
 def groupnorm(x: torch.Tensor, gamma, beta, eps: float, rows_per_stat: int, *, x2=None, silu=False, groups=32,
-              out=None):
+              out=None, relu=False, residual: Optional[torch.Tensor] = None):
+    """y = act(GroupNorm(x) [+ residual]); act SiLU (``silu``) or ReLU (``relu``)."""
     lib = _lib.load()
     _need(x, torch.bfloat16, "groupnorm x")
     M = x.shape[0]
@@ -282,7 +283,14 @@ def groupnorm(x: torch.Tensor, gamma, beta, eps: float, rows_per_stat: int, *, x
     d.C1 = C1
     d.M, d.C, d.G, d.rows_per_stat = M, C, groups, rows_per_stat
     d.gamma, d.beta, d.eps = gamma.data_ptr(), beta.data_ptr(), float(eps)
-    d.silu = int(silu)
+    if silu and relu:
+        raise _lib.ActhError("groupnorm: silu and relu are exclusive")
+    d.silu = 2 if relu else int(silu)
+    if residual is not None:
+        _need(residual, torch.bfloat16, "groupnorm residual")
+        if residual.shape[0] < M or residual.shape[1] < C:
+            raise _lib.ActhError(f"groupnorm: residual {tuple(residual.shape)} too small for ({M}, {C})")
+        d.res, d.ldres = residual.data_ptr(), _rows(residual, "groupnorm residual")
     d.y, d.ldy = out.data_ptr(), _rows(out, "groupnorm out")
     d.ws = ws.data_ptr()
     _lib.check(lib.acth_groupnorm(ctypes.byref(d), _stream()), "acth_groupnorm")
@@ -439,6 +447,37 @@ def im2col3x3(x: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
     K = 9 * C
     out = torch.empty((B * H * W, K), device=x.device, dtype=torch.bfloat16)
     _lib.check(lib.acth_im2col3x3(_p(x.contiguous()), B, H, W, C, _p(out), K, _stream()), "acth_im2col3x3")
+    return out
+
+
+def im2col(x: torch.Tensor, B: int, H: int, W: int, kh: int, kw: int, stride: int, pad: int,
+           kpad: Optional[int] = None) -> torch.Tensor:
+    """NHWC rows (B*H*W, C) -> (B*Ho*Wo, Kpad) patches, column (ky*kw + kx)*C + c, zero-padded to Kpad
+    (default: kh*kw*C rounded up to a multiple of 8)."""
+    lib = _lib.load()
+    _need(x, torch.bfloat16, "im2col x")
+    C = x.shape[1]
+    if x.shape[0] != B * H * W:
+        raise _lib.ActhError(f"im2col: x has {x.shape[0]} rows, expected {B * H * W}")
+    Ho, Wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    K = kh * kw * C
+    kp = (K + 7) // 8 * 8 if kpad is None else kpad
+    out = torch.empty((B * Ho * Wo, kp), device=x.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_im2col(_p(x), _rows(x, "im2col x"), B, H, W, C, kh, kw, stride, pad, Ho, Wo, _p(out), kp,
+                               _stream()), "acth_im2col")
+    return out
+
+
+def maxpool2d(x: torch.Tensor, B: int, H: int, W: int, k: int, stride: int, pad: int) -> torch.Tensor:
+    lib = _lib.load()
+    _need(x, torch.bfloat16, "maxpool x")
+    C = x.shape[1]
+    if x.shape[0] != B * H * W:
+        raise _lib.ActhError(f"maxpool: x has {x.shape[0]} rows, expected {B * H * W}")
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    out = torch.empty((B * Ho * Wo, C), device=x.device, dtype=torch.bfloat16)
+    _lib.check(lib.acth_maxpool2d(_p(x), _rows(x, "maxpool x"), B, H, W, C, k, stride, pad, Ho, Wo, _p(out),
+                                  _rows(out, "maxpool out"), _stream()), "acth_maxpool2d")
     return out
 
 

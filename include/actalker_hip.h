@@ -100,7 +100,9 @@ typedef struct ActhLayerNormDesc {
 } ActhLayerNormDesc;
 int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream);
 
-/* ---- GroupNorm(G) (+SiLU), stats over rows_per_stat tokens, optional channel-concat input */
+/* ---- GroupNorm(G), stats over rows_per_stat tokens, optional channel-concat input;
+ * y = act(GN(x) + res): act (field `silu`) 0 none, 1 SiLU, 2 ReLU; res (bf16 rows, C channels) optional
+ * (ResNet-GN blocks of the VASA encoders, vasa_feature_v2.py:64-85 / 129-150) */
 typedef struct ActhGroupNormDesc {
   const void* x; int ldx; const void* x2; int ldx2; int C1;
   int M, C, G, rows_per_stat;
@@ -108,6 +110,7 @@ typedef struct ActhGroupNormDesc {
   int silu;
   void* y; int ldy;
   double* ws;
+  const void* res; int ldres;
 } ActhGroupNormDesc;
 int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream);
 size_t acth_groupnorm_workspace_size(int M, int C, int G, int rows_per_stat);
@@ -176,6 +179,10 @@ int acth_nchw_to_tokens(const void* x, int in_dt, void* y, int out_dt, int ldy, 
 int acth_tokens_to_nchw(const void* x, int in_dt, int ldx, void* y, int out_dt, int B, int C, int HW,
                         hipStream_t stream);
 int acth_im2col3x3(const void* x, int B, int H, int W, int C, void* out, int Kpad, hipStream_t stream);
+int acth_im2col(const void* x, int ldx, int B, int H, int W, int C, int kh, int kw, int stride, int pad,
+                int Ho, int Wo, void* out, int Kpad, hipStream_t stream);
+int acth_maxpool2d(const void* x, int ldx, int B, int H, int W, int C, int k, int stride, int pad, int Ho, int Wo,
+                   void* y, int ldy, hipStream_t stream);
 int acth_gather_rows(const void* src, int lds, int Ls, const int* idx, int n, void* dst, int ldd, int Ld,
                      int nb, int C, hipStream_t stream);
 int acth_frame_mean(const void* x, int ldx, int B, int F, int T, int C, void* out, int ldo,

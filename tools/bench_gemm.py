@@ -11,17 +11,21 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from actalker_amd import ops  # noqa: E402
 
-# (mode, M, N, K, act) — from bench.py ACTH_GEMM_STATS at 576x1024, 56-frame calls
+# (mode, M, N, K, act) — bench.py ACTH_GEMM_STATS at 576x1024, 84-frame calls (profiles/r2_step0_gemm_shapes.log),
+# ordered by their share of the mode-0 step
 SHAPES = [
-    ("dense", 516096, 2560, 320, 2), ("dense", 129024, 5120, 640, 2), ("dense", 516096, 320, 320, 0),
-    ("dense", 32256, 10240, 1280, 2), ("dense", 516096, 320, 1280, 0), ("conv", 516096, 320, 2880, 0),
-    ("dense", 129024, 640, 640, 0), ("dense", 129024, 640, 2560, 0), ("conv", 32256, 1280, 11520, 0),
-    ("temporal", 516096, 320, 960, 0), ("conv", 129024, 640, 5760, 0), ("dense", 32256, 1280, 5120, 0),
-    ("dense", 516096, 960, 320, 0), ("dense", 32256, 1280, 1280, 0), ("conv", 8064, 1280, 11520, 0),
+    ("dense", 774144, 2560, 320, 2), ("dense", 193536, 5120, 640, 2), ("dense", 48384, 10240, 1280, 2),
+    ("dense", 774144, 320, 320, 0), ("dense", 774144, 320, 1280, 0), ("conv", 774144, 320, 2880, 0),
+    ("dense", 193536, 640, 640, 0), ("dense", 193536, 640, 2560, 0), ("dense", 774144, 960, 320, 0),
+    ("dense", 48384, 1280, 5120, 0), ("conv", 48384, 1280, 11520, 0), ("conv", 193536, 640, 5760, 0),
+    ("dense", 48384, 1280, 1280, 0), ("temporal", 774144, 320, 960, 0), ("dense", 193536, 1920, 640, 0),
+    ("dense", 774144, 640, 320, 0), ("conv", 12096, 1280, 11520, 0),
     # reference points (not UNet shapes): square 4096^3 / 8192^3 (operands L2 / MALL resident),
     # and a 2048-wide K = 4096 panel streaming a 1 GB A from HBM
     ("dense", 4096, 4096, 4096, 0), ("dense", 8192, 8192, 8192, 0), ("dense", 131072, 2048, 4096, 0),
 ]
+CONV_HW = {774144: (72, 128), 193536: (36, 64), 48384: (18, 32), 12096: (9, 16),
+           516096: (72, 128), 129024: (36, 64), 32256: (18, 32), 8064: (9, 16)}
 
 
 def run(mode, M, N, K, act, tile, iters, dev, sink=False, residual=False):
@@ -29,14 +33,14 @@ def run(mode, M, N, K, act, tile, iters, dev, sink=False, residual=False):
     kw = {}
     if mode == "conv":
         cin = K // 9
-        H, W = (72, 128) if M == 516096 else (36, 64) if M == 129024 else (18, 32) if M == 32256 else (9, 16)
+        H, W = CONV_HW[M]
         B = M // (H * W)
         a = torch.randn(B * H * W, cin, generator=g).to(dev, torch.bfloat16)
         kw["conv"] = dict(H=H, W=W, Ho=H, Wo=W, stride=1, upsample=False, B=B)
     elif mode == "temporal":
         cin = K // 3
         a = torch.randn(M, cin, generator=g).to(dev, torch.bfloat16)
-        kw["temporal"] = dict(F=14, S=M // 56)
+        kw["temporal"] = dict(F=14, S=9216 if M in (774144, 516096) else 2304 if M in (193536, 129024) else 576)
     else:
         a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
     w = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev, torch.bfloat16)

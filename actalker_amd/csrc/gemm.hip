@@ -179,16 +179,27 @@ int gemm256_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a
 int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                   int vec_ok, hipStream_t stream);
 
-// Tile choice (measured on MI355X, tools/bench_gemm.py): the phased 256x320 kernel for every
-// non-GEGLU GEMM that fills the chip (every UNet width is a multiple of 320), the phased 256x256
-// kernel for GEGLU (its wave tiles hold whole hidden|gate granule pairs), the persistent 256x160
-// kernel for grids too small for either, the 128x128 kernel for small M or N.
+// Tile choice (measured on MI355X, tools/bench_gemm.py, profiles/r2_step3_bench_gemm_tiles.log): the
+// phased 256x256 kernel for GEGLU (its wave tiles hold whole hidden|gate granule pairs); otherwise
+// whichever phased tile (256x320 or 256x256) wastes less of the machine -- the fraction of its
+// columns that are real (N / padded N) times the fraction of its last round of tiles over the CUs
+// that is occupied -- provided that is >= 0.7 (e.g. 774144x320: 256x320; 12096x1280 and 4096^2:
+// 256x256, +18-60 % over the alternatives); the persistent 256x160 kernel for grids too small for
+// either, the 128x128 kernel for small M or N.
+static double tile_eff(long long mt, int N, int bn) {
+  const long long nt = (N + bn - 1) / bn, t = mt * nt;
+  const long long rounds = (t + 255) / 256;
+  return (double)N / (double)(nt * bn) * (double)t / (double)(rounds * 256);
+}
+
 static int choose_tile(const ActhGemmDesc* d) {
   if (d->tile & 0xff) return d->tile & 0xff;
   if (d->N < 128 || d->M < 256) return 1;
   const long long mt = (d->M + 255) / 256;
-  if (d->act == 2) return (d->N % 256 == 0 && mt * (d->N / 256) >= 256) ? 4 : 1;
-  if (mt * ((d->N + 319) / 320) >= 256) return 5;
+  if (d->act == 2) return (d->N % 256 == 0 && mt * (d->N / 256) >= 192) ? 4 : 1;
+  const double e5 = tile_eff(mt, d->N, 320), e4 = tile_eff(mt, d->N, 256);
+  if (e5 >= 0.7 && e5 >= e4) return 5;
+  if (e4 >= 0.7) return 4;
   return 3;
 }
 

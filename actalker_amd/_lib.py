@@ -146,6 +146,7 @@ SIGNATURES = {
                      c_vp], c_int),
     "acth_maxpool2d": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
                         c_vp], c_int),
+    "acth_debug_gemm_stamps": ([c_vp, c_int], c_int),
     "acth_groupnorm": ([_P(GroupNormDesc), c_vp], c_int),
     "acth_groupnorm_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
     "acth_mamba_combine_ln": ([_P(MambaCombineDesc), c_vp], c_int),

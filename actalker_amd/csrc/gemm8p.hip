@@ -17,6 +17,8 @@
 // of each half) one wave's ds_read + DMA issue segment overlaps the other's MFMA segment. Hazards
 // under the stagger (one barrier = half a phase): a half-tile is read >= one phase after the last
 // wait that retires it; a buffer is re-staged >= two phases after its last read.
+#include <type_traits>
+
 #include "gemm_common.h"
 
 using namespace gemm;
@@ -72,6 +74,12 @@ __device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, const RowPk& ri
   return r.a + (tap - 1) * p.S;
 }
 
+// In-kernel phase stamps (tile bit 0x400, diagnostics only): s_memtime at kernel entry, after the
+// prologue wait, after the main loop and at the end of the epilogue, per workgroup
+// (tools/gemm_stamps.py reads them back through acth_debug_gemm_stamps).
+#define STAMP_WGS 16384
+__device__ unsigned long long g_gemm_stamps[STAMP_WGS * 4];
+
 #define BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
                    __builtin_amdgcn_sched_barrier(0); } while (0)
 
@@ -107,6 +115,12 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave % WR, wc = wave / WR;     // wave's row / column slot inside a quadrant
+  const bool stamps = (p.tile & 0x400) != 0;
+  const int stamp_wg = blockIdx.x + gridDim.x * blockIdx.y;
+  auto stamp = [&](int k) {
+    if (stamps && tid == 0 && stamp_wg < STAMP_WGS) g_gemm_stamps[stamp_wg * 4 + k] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   const bool late = wave >= 4;                  // staggered half
   // B-half DMA pieces this wave issues (wave + 8u < NBP): the count differs by wave when NBP % 8
   const int nbw = (NBP - wave + 7) / 8;
@@ -281,6 +295,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   BAR();
+  stamp(1);
   if (late) BAR();
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -323,6 +338,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   if (!late) BAR();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   BAR();
+  stamp(2);
 
   if (p.tile & 0x100) {                          // diagnostic: main loop only (keeps acc live)
 #pragma unroll
@@ -435,11 +451,132 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
         }
       }
     };
-    slab(acc[0][0]); flush(0, 0);
-    slab(acc[0][1]); flush(0, 1);
-    slab(acc[1][0]); flush(1, 0);
-    slab(acc[1][1]); flush(1, 1);
+    // Fast path for the UNet's residual-stream / conv epilogues (no activation, bf16 out, identity row
+    // map, 16-byte aligned rows, whole 8-column chunks, residual without a row map, row bias staged in
+    // LDS): the combination of bias / row bias / residual / mix is a compile-time choice, so the chunk
+    // loop is branch-free, and each lane keeps one 8-column chunk across the quadrant's rows (its bias
+    // chunk in registers, row-strided pointers) instead of re-deriving 64-bit addresses per chunk.
+    // Measured with tools/gemm_stamps.py: the generic loop spent ~29k cycles per 256x320 tile.
+    const bool fast = p.act == 0 && !p.out_f32 && p.orow_div >= p.M && vec_ok && (p.N & 7) == 0 && !p.rmap &&
+                      (!p.rowbias || rb_lds);
+    auto fast_epilogue = [&](auto res_c, auto mix_c, auto rb_c) {
+      constexpr bool RES = decltype(res_c)::value, MIXB = decltype(mix_c)::value, RB = decltype(rb_c)::value;
+      constexpr int RPI = 64 / CPR, LPI = RPI * CPR, NIT = (SR + RPI - 1) / RPI;
+      // residual double-buffered across quadrants; with a mix operand too the registers allow one buffer
+      constexpr int NRB = (RES && !MIXB) ? 2 : 1, NMB = MIXB ? 1 : 0;
+      const int r0 = lane / CPR, c8 = (lane - r0 * CPR) * 8;
+      const bool lane_ok = lane < LPI;
+      const size_t step_c = (size_t)RPI * p.ldc, step_r = (size_t)RPI * p.ldr, step_m = (size_t)RPI * p.ldmix;
+      auto q_col = [&](int qn) { return tile_n + qn * (BN_ / 2) + wc * SC + c8; };
+      auto q_row = [&](int qm) { return tile_m + qm * 128 + wr * SR + r0; };
+      auto ld_ok = [&](int rowf, int col, int it) {
+        return lane_ok && col < p.N && r0 + it * RPI < SR && rowf + it * RPI < p.M;
+      };
+      // a quadrant's residual (mix) chunks for every iteration, issued together: the residual of the
+      // next quadrant is in flight while this one is processed (the chunk loop was HBM-latency bound
+      // with one chunk of look-ahead: ~49k cycles per tile). Invalid (row, column) slots read the
+      // tensor's first chunk instead (never used), so the loads are unconditional.
+      uint4 rbuf[NRB][NIT], mbuf[NMB > 0 ? NMB : 1][NIT];
+      auto load_res = [&](int qm, int qn, uint4 (&dst)[NIT]) {
+        const int rowf = q_row(qm), col = q_col(qn);
+        const bf16_t* rp = (const bf16_t*)p.R + (size_t)rowf * p.ldr + col;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it)
+          dst[it] = *reinterpret_cast<const uint4*>(ld_ok(rowf, col, it) ? rp + it * step_r : (const bf16_t*)p.R);
+      };
+      auto load_mix = [&](int qm, int qn, uint4 (&dst)[NIT]) {
+        const int rowf = q_row(qm), col = q_col(qn);
+        const bf16_t* mp = (const bf16_t*)p.MIX + (size_t)rowf * p.ldmix + col;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it)
+          dst[it] = *reinterpret_cast<const uint4*>(ld_ok(rowf, col, it) ? mp + it * step_m : (const bf16_t*)p.MIX);
+      };
+      auto one = [&](int qm, int qn, const uint4 (&rq)[NIT], const uint4 (&mq)[NIT]) {
+        const int lc0 = qn * (BN_ / 2) + wc * SC;
+        const int col = q_col(qn), rowf = q_row(qm);
+        const float4 b0 = *reinterpret_cast<const float4*>(&sbias[lc0 + c8]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&sbias[lc0 + c8 + 4]);
+        bf16_t* cp = (bf16_t*)p.C + (size_t)(rowf + p.orow_off) * p.ldc + col;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int r = r0 + it * RPI;
+          const int rr = r < SR ? r : 0;
+          const float4 x0 = *reinterpret_cast<const float4*>(&et[rr * EPI_LD + c8]);
+          const float4 x1 = *reinterpret_cast<const float4*>(&et[rr * EPI_LD + c8 + 4]);
+          float v[8];
+          v[0] = fmaf(x0.x, p.alpha, b0.x); v[1] = fmaf(x0.y, p.alpha, b0.y);
+          v[2] = fmaf(x0.z, p.alpha, b0.z); v[3] = fmaf(x0.w, p.alpha, b0.w);
+          v[4] = fmaf(x1.x, p.alpha, b1.x); v[5] = fmaf(x1.y, p.alpha, b1.y);
+          v[6] = fmaf(x1.z, p.alpha, b1.z); v[7] = fmaf(x1.w, p.alpha, b1.w);
+          if (RB) {
+            const int row = rowf + it * RPI;
+            const int img = min(max(udiv22(row < p.M ? row : p.M - 1, p.rb_div) - rb_img0, 0), RB_IMG - 1);
+            const float4 q0 = *reinterpret_cast<const float4*>(&srb[img * BN_ + lc0 + c8]);
+            const float4 q1 = *reinterpret_cast<const float4*>(&srb[img * BN_ + lc0 + c8 + 4]);
+            v[0] += q0.x; v[1] += q0.y; v[2] += q0.z; v[3] += q0.w;
+            v[4] += q1.x; v[5] += q1.y; v[6] += q1.z; v[7] += q1.w;
+          }
+          if (RES) {
+            float t[8];
+            unpack8(rq[it], t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += t[e];
+          }
+          if (MIXB) {
+            float t[8];
+            unpack8(mq[it], t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = p.mix_alpha * t[e] + (1.0f - p.mix_alpha) * v[e];
+          }
+          if (ld_ok(rowf, col, it)) *reinterpret_cast<uint4*>(cp + it * step_c) = pack8(v);
+        }
+      };
+      constexpr int QM[4] = {0, 0, 1, 1}, QN[4] = {0, 1, 0, 1};
+      if (RES && NRB == 2) load_res(0, 0, rbuf[0]);
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        if (RES && NRB == 2 && qi + 1 < 4) load_res(QM[qi + 1], QN[qi + 1], rbuf[(qi + 1) % NRB]);
+        if (RES && NRB == 1) load_res(QM[qi], QN[qi], rbuf[0]);
+        if (MIXB) load_mix(QM[qi], QN[qi], mbuf[0]);
+        slab(acc[QM[qi]][QN[qi]]);
+        one(QM[qi], QN[qi], rbuf[qi % NRB], mbuf[0]);
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (fast) {
+      const int sel = (p.R ? 1 : 0) | (p.MIX ? 2 : 0) | (p.rowbias ? 4 : 0);
+      switch (sel) {
+        case 0: fast_epilogue(F_{}, F_{}, F_{}); break;
+        case 1: fast_epilogue(T_{}, F_{}, F_{}); break;
+        case 3: fast_epilogue(T_{}, T_{}, F_{}); break;
+        case 4: fast_epilogue(F_{}, F_{}, T_{}); break;
+        default:
+          slab(acc[0][0]); flush(0, 0);
+          slab(acc[0][1]); flush(0, 1);
+          slab(acc[1][0]); flush(1, 0);
+          slab(acc[1][1]); flush(1, 1);
+      }
+    } else {
+      slab(acc[0][0]); flush(0, 0);
+      slab(acc[0][1]); flush(0, 1);
+      slab(acc[1][0]); flush(1, 0);
+      slab(acc[1][1]); flush(1, 1);
+    }
   }
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(3);
+  }
+}
+
+extern "C" int acth_debug_gemm_stamps(unsigned long long* host_dst, int n_wgs) {
+  if (!host_dst || n_wgs <= 0 || n_wgs > STAMP_WGS) return ACTH_EINVAL;
+  if (hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_gemm_stamps), (size_t)n_wgs * 4 * sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return ACTH_ELAUNCH;
+  return ACTH_OK;
 }
 
 template <int BN_>

@@ -196,6 +196,9 @@ int acth_cfg_euler_accum(const float* noise, const long long* unit_off, const fl
                          int F, int S, hipStream_t stream);
 int acth_div_counter(const float* acc, const float* cnt, float* out, int T, int S, hipStream_t stream);
 int acth_version(void);
+/* diagnostics: per-workgroup s_memtime phase stamps of the last phased-GEMM launch made with tile bit
+ * 0x400 (entry, prologue landed, main loop done, epilogue done), n_wgs x 4 values copied to host */
+int acth_debug_gemm_stamps(unsigned long long* host_dst, int n_wgs);
 
 #ifdef __cplusplus
 }

@@ -115,7 +115,7 @@ def test_gemm_grouped_raster(dev, tile, gm):
 
 
 @pytest.mark.parametrize("tile", [4, 5])
-@pytest.mark.parametrize("case", ["plain", "rmap_mix_silu", "ragged_n"])
+@pytest.mark.parametrize("case", ["plain", "rmap_mix_silu", "ragged_n", "res_mix", "bias_only", "rowbias", "rb_res"])
 def test_gemm_phased_vector_residual(dev, tile, case):
     """The phased kernels' vector residual path (16-byte-aligned residual rows, the residual chunk
     loaded one iteration ahead, invalid rows / columns clamped to row 0): N a multiple of 8, a
@@ -136,6 +136,21 @@ def test_gemm_phased_vector_residual(dev, tile, case):
         rows = torch.arange(M)
         rr = rmap[rows // r_div].long() * r_div + rows % r_div
         refo = 0.3 * mix.float() + 0.7 * F.silu(a.float() @ w.float().t() + bias + res.float()[rr])
+    elif case in ("res_mix", "bias_only", "rowbias", "rb_res"):
+        # the fast-path epilogue combinations (compile-time bias / row bias / residual / mix choice)
+        res, mix, rowb = bf(rnd(M, N)), bf(rnd(M, N)), rnd(-(-M // 700), N)
+        kw = dict(bias=bias.to(dev))
+        refo = a.float() @ w.float().t() + bias
+        if case in ("res_mix", "rb_res"):
+            kw["residual"] = res.to(dev)
+            refo = refo + res.float()
+        if case in ("rowbias", "rb_res"):
+            kw.update(rowbias=rowb.to(dev), rb_div=700)
+            refo = refo + rowb.repeat_interleave(700, 0)[:M]
+        if case == "res_mix":
+            kw.update(mix=mix.to(dev), mix_alpha=0.3)
+            refo = 0.3 * mix.float() + 0.7 * refo
+        out = ops.gemm(a.to(dev), w.to(dev), tile=tile, **kw)
     else:
         res = bf(rnd(M, N))
         out = ops.gemm(a.to(dev), w.to(dev), bias=bias.to(dev), residual=res.to(dev), tile=tile)

@@ -1,0 +1,50 @@
+"""Where a phased-GEMM workgroup's time goes: per-workgroup s_memtime stamps (tile bit 0x400) at entry,
+after the prologue's K tile 0 has landed, after the main loop and after the epilogue, for the
+bench_gemm shapes. Prints per-phase mean cycles per workgroup and the kernel's wall time.
+
+  python tools/gemm_stamps.py [--only 0,3] [--residual]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from actalker_amd import _lib, ops  # noqa: E402
+from tools.bench_gemm import SHAPES, run  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="0,3,4,5")
+    ap.add_argument("--residual", action="store_true")
+    ap.add_argument("--tile", type=int, default=0)
+    ap.add_argument("--sink", action="store_true", help="every row block writes the same 256 output rows")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    lib = _lib.load()
+    for idx in [int(i) for i in a.only.split(",")]:
+        mode, M, N, K, act = SHAPES[idx]
+        tf, ms = run(mode, M, N, K, act, a.tile, 5, dev, sink=a.sink, residual=a.residual)
+        tf2, ms2 = run(mode, M, N, K, act, a.tile | 0x400, 1, dev, sink=a.sink, residual=a.residual)
+        mt = (M + 255) // 256
+        nt = -(-N // 320) if (a.tile or 5) == 5 and act != 2 else -(-N // 256)
+        n = min(mt * nt, 16384)
+        buf = (ctypes.c_ulonglong * (4 * n))()
+        _lib.check(lib.acth_debug_gemm_stamps(buf, n), "stamps")
+        st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.float64)
+        ok = (st[:, 3] > st[:, 0]) & (st[:, 0] > 0)
+        st = st[ok]
+        d = np.diff(st, axis=1)
+        tot = st[:, 3] - st[:, 0]
+        print(f"{mode} {M}x{N}x{K} act {act}{' +res' if a.residual else ''}{' sink' if a.sink else ''}: {ms:.3f} ms ({tf:.0f} TF/s), "
+              f"stamped {ms2:.3f} ms; {len(st)} WGs; cycles/WG mean: prologue {d[:, 0].mean():.0f}, "
+              f"main {d[:, 1].mean():.0f}, epilogue {d[:, 2].mean():.0f}, total {tot.mean():.0f} "
+              f"(median {np.median(tot):.0f}, p90 {np.percentile(tot, 90):.0f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()

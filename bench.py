@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s achievable)
 TFLOP_PER_FRAME_FWD = 3.433        # SURVEY.md 8(d), 576x1024, mode 2 (modes 0/1: 3.402)
 MODES = {0: ([1, 0], "mode=0 audio-only"), 1: ([0, 1], "mode=1 expression-only"), 2: ([1, 1], "mode=2 audio+expression")}
 
@@ -183,6 +184,77 @@ class GemmTimer:
         return "\n".join(lines)
 
 
+class FamilyTimer:
+    """HIP events around every launch of the non-GEMM kernel families on the launch stream inside the
+    timed region, with each launch's algorithmic work: flash attention FLOPs (4 S^2 64 per head and
+    batch), selective-scan bytes (u read once for both directions, the fp32 xdbl rows, both outputs
+    written), GroupNorm / LayerNorm bytes (input read once, output written once -- the stats pass's
+    second read of the input is the kernels' cost, not the algorithm's)."""
+
+    def __init__(self):
+        self.ev = {}                         # family -> list of (e0, e1, work)
+
+    def _wrap(self, mod, name, fam, work_fn):
+        orig = getattr(mod, name)
+
+        def timed(*a, **k):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            out = orig(*a, **k)
+            e1.record()
+            self.ev.setdefault(fam, []).append((e0, e1, work_fn(*a, **k)))
+            return out
+        setattr(mod, name, timed)
+        self._restore.append((mod, name, orig))
+
+    def install(self):
+        from actalker_amd import ops
+        import actalker_amd.modules as mods
+        self._restore = []
+
+        def w_flash(qkv, nbatch, S, heads, out=None):
+            return 4.0 * nbatch * heads * S * S * 64
+
+        def w_scan(u, xdbl, *a, nb, L, R, n_keep, **k):
+            D = u.shape[1]
+            return nb * L * D * 2 + nb * L * xdbl.shape[1] * 4 + 2 * nb * n_keep * D * 2
+
+        def w_gn(x, *a, x2=None, residual=None, **k):
+            C = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
+            return 2.0 * x.shape[0] * C * 2 + (x.shape[0] * C * 2 if residual is not None else 0)
+
+        def w_ln(x, *a, add=None, sum_out=None, **k):
+            return 2.0 * x.numel() * 2 + (x.numel() * 2 if sum_out is not None else 0)
+
+        self._wrap(ops, "flash_attn", "flash_attn", w_flash)
+        self._wrap(ops, "selective_scan", "selective_scan", w_scan)
+        self._wrap(ops, "groupnorm", "groupnorm", w_gn)
+        self._wrap(ops, "layernorm", "layernorm", w_ln)
+        mods.ops = ops
+        return self
+
+    def uninstall(self):
+        for mod, name, orig in self._restore:
+            setattr(mod, name, orig)
+
+    def report(self, step_ms_total):
+        peak = {"flash_attn": ("mfma", PEAK_BF16_TFLOPS, "TFLOP/s", 1e12),
+                "selective_scan": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
+                "groupnorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
+                "layernorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9)}
+        out = {}
+        for fam, evs in self.ev.items():
+            ms = sum(a.elapsed_time(b) for a, b, _ in evs)
+            work = sum(w for _, _, w in evs)
+            bound, pk, unit, scale = peak[fam]
+            ach = work / (ms / 1e3) / scale
+            out[fam] = dict(bound=bound, achieved=round(ach, 1), peak=pk, unit=unit, frac=round(ach / pk, 4),
+                            launches=len(evs), avg_launch_us=round(1000.0 * ms / len(evs), 1),
+                            share_of_step=round(ms / step_ms_total, 4))
+        return out
+
+
 def cpu_baseline(unet, H, W, frames=2, mode=0):
     """Oracle (fp32 CPU restatement) on a bounded sample: one UNet call, 1 CFG branch x `frames`
     frames at full resolution; frames/s extrapolated to the N=14 workload (200 frame-forwards
@@ -237,6 +309,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
+    ap.add_argument("--no-four-branch-compare", action="store_true",
+                    help="skip the extra timed run with all 4 CFG branches evaluated (reported beside the headline)")
     ap.add_argument("--units-per-call", type=int, default=0,
                     help="(window, branch) units per UNet call; 0 = auto (fewest calls within the kernels' "
                          "2 GiB buffer extents; the reference's call is 4 units = 56 frames)")
@@ -287,6 +361,7 @@ def main():
     with torch.no_grad():
         pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.warmup)
     timer = None if args.no_roofline else GemmTimer().install()
+    ftimer = None if args.no_roofline else FamilyTimer().install()
     barrier()
     t_start = time.perf_counter()
     with torch.no_grad():
@@ -295,6 +370,8 @@ def main():
     elapsed = time.perf_counter() - t_start
     if timer is not None:
         timer.uninstall()
+    if ftimer is not None:
+        ftimer.uninstall()
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev)
@@ -323,6 +400,22 @@ def main():
                     kernel_share_of_step=round(gemm_ms / (elapsed * 1000.0), 3))
     n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank, branches=branches)[0])
     frame_fwds = n_units_rank * fpb * args.steps
+    # the reference-shaped figure: all four CFG branches evaluated (no twin-branch elimination), same steps
+    four = None
+    if twins and world == 1 and not args.no_four_branch_compare:
+        cfg4 = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7,
+                             concurrent_calls=args.concurrent_calls, dedup_branches=False,
+                             units_per_call=args.units_per_call)
+        with torch.no_grad():
+            pl.denoise(backend, inp["latents"], cfg4, rank, world, group, steps=1)
+        barrier()
+        t4 = time.perf_counter()
+        with torch.no_grad():
+            pl.denoise(backend, inp["latents"], cfg4, rank, world, group, steps=args.steps)
+        barrier()
+        e4 = time.perf_counter() - t4
+        four = dict(value=round(N / (cfg.num_inference_steps * e4 / args.steps), 4),
+                    ms_per_step=round(1000.0 * e4 / args.steps, 2), cfg_branches_evaluated=4)
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(unet, H, W, frames=args.cpu_frames, mode=args.mode)
@@ -342,10 +435,12 @@ def main():
             "unet_frame_forwards_per_s_per_gpu": round(frame_fwds / elapsed, 3),
             "achieved_mfma_tflops_whole_step": round(frame_fwds * TFLOP_PER_FRAME_FWD / elapsed, 1),
             "cfg_branches_evaluated": len(branches),
+            "all_four_branches": four,
             "finite": ok,
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
+            "kernel_families": (ftimer.report(elapsed * 1000.0) if ftimer is not None else None),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -72,6 +72,18 @@ class IpAttnDesc(ctypes.Structure):
     ]
 
 
+class FfnDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_int),
+        ("w1", c_vp), ("ldw1", c_int), ("b1", c_vp),
+        ("w2", c_vp), ("ldw2", c_int), ("b2", c_vp),
+        ("res", c_vp), ("ldres", c_int),
+        ("mix", c_vp), ("ldmix", c_int), ("mix_alpha", c_float),
+        ("y", c_vp), ("ldy", c_int),
+        ("M", c_int), ("C", c_int),
+    ]
+
+
 class LayerNormDesc(ctypes.Structure):
     _fields_ = [
         ("x", c_vp), ("ldx", c_int),
@@ -138,6 +150,8 @@ _P = ctypes.POINTER
 SIGNATURES = {
     "acth_gemm": ([_P(GemmDesc), c_vp], c_int),
     "acth_gemm_desc_size": ([], c_int),
+    "acth_geglu_ffn": ([_P(FfnDesc), c_vp], c_int),
+    "acth_debug_ffn_stamps": ([c_vp, c_int, c_int], c_int),
     "acth_flash_attn": ([_P(AttnDesc), c_vp], c_int),
     "acth_temporal_attn": ([_P(TemporalAttnDesc), c_vp], c_int),
     "acth_ip_attn": ([_P(IpAttnDesc), c_vp], c_int),

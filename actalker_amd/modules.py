@@ -23,6 +23,7 @@ Reference map (file:line under /root/reference/src/models/base unless noted):
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -82,6 +83,24 @@ def pack_geglu(w: torch.Tensor, b: torch.Tensor):
     wi = torch.stack([hw.view(inner // G, G, -1), gw.view(inner // G, G, -1)], 1).reshape(2 * inner, -1)
     bi = torch.stack([hb.view(inner // G, G), gb.view(inner // G, G)], 1).reshape(-1)
     return _bf(wi), _f32(bi)
+
+
+def ffn_w2_perm(inner: int) -> torch.Tensor:
+    """Column order of the fused feed-forward's W2 (acth_geglu_ffn): within each 32-unit hidden chunk,
+    column 8q + j holds unit 4q + j (j < 4) or 16 + 4q + (j - 4) -- the order in which a lane of the
+    up-projection's 16x16 MFMA fragments holds the gated units (rows 4q..4q+3 of the two granules)."""
+    q, j = torch.arange(4).view(4, 1), torch.arange(8).view(1, 8)
+    local = torch.where(j < 4, 4 * q + j, 16 + 4 * q + (j - 4)).reshape(32)
+    return (torch.arange(0, inner, 32).view(-1, 1) + local.view(1, 32)).reshape(-1)
+
+
+def pack_ffn_w2(w: torch.Tensor) -> torch.Tensor:
+    """FeedForward output Linear (C, I) -> columns permuted by ffn_w2_perm, times 0.5 (the kernel
+    carries 2 h gelu(g); scaling by a power of two is exact in bf16)."""
+    return _bf(0.5 * w[:, ffn_w2_perm(w.shape[1]).to(w.device)].float())
+
+
+FUSED_FFN = os.environ.get("ACTH_FUSED_FFN", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------
@@ -396,7 +415,7 @@ class GEGLU(Packed):
         return self._pk("geglu", lambda: pack_geglu(self.proj.weight, self.proj.bias))
 
 
-class FeedForward(nn.Module):
+class FeedForward(Packed):
     def __init__(self, dim, dim_out=None, mult=4, dropout=0.0, activation_fn="geglu", final_dropout=False,
                  inner_dim=None, bias=True):
         super().__init__()
@@ -405,10 +424,20 @@ class FeedForward(nn.Module):
         self.net = nn.ModuleList([GEGLU(dim, inner_dim, bias=bias), nn.Dropout(dropout),
                                   Linear(inner_dim, dim_out, bias=bias)])
 
-    def run(self, n, residual):
+    def fusable(self, C: int) -> bool:
+        out = self.net[2]
+        return (FUSED_FFN and C in ops.FFN_FUSED_C and out.in_features == 4 * C and out.out_features == C
+                and self.net[0].proj.in_features == C)
+
+    def run(self, n, residual, mix=None, mix_alpha: float = 0.0):
+        """net[2](GEGLU(n)) + residual [AlphaBlender with ``mix``]; one fused kernel at C = 320."""
         w, b = self.net[0].packed()
+        if self.fusable(n.shape[1]):
+            w2 = self._pk("w2perm", lambda: pack_ffn_w2(self.net[2].weight))
+            return ops.geglu_ffn(n, w, b, w2, self.net[2].b(), residual=residual, mix=mix, mix_alpha=mix_alpha)
         g = ops.gemm(n, w, bias=b, act=ops.ACT_GEGLU)
-        return ops.gemm(g, self.net[2].w(), bias=self.net[2].b(), residual=residual)
+        return ops.gemm(g, self.net[2].w(), bias=self.net[2].b(), residual=residual, mix=mix,
+                        mix_alpha=mix_alpha)
 
 
 class BasicTransformerBlock(nn.Module):
@@ -456,10 +485,7 @@ class TemporalBasicTransformerBlock(nn.Module):
         n = ops.layernorm(t, *self.norm2.gb(), self.norm2.eps, out=n)
         t = self.attn2.run_cross(ctx, n, t, S, temporal=True)
         n = ops.layernorm(t, *self.norm3.gb(), self.norm3.eps, out=n)
-        w, b = self.ff.net[0].packed()
-        g = ops.gemm(n, w, bias=b, act=ops.ACT_GEGLU)
-        return ops.gemm(g, self.ff.net[2].w(), bias=self.ff.net[2].b(), residual=t, mix=h_spatial,
-                        mix_alpha=mix_alpha)
+        return self.ff.run(n, t, mix=h_spatial, mix_alpha=mix_alpha)
 
 
 # ------------------------------------------------------------------------------------------

@@ -242,6 +242,53 @@ def ip_attn(vbase: torch.Tensor, M: int, heads: int, rows_per_ctx: int, S: int, 
 
 
 # ------------------------------------------------------------------------------------------
+FFN_FUSED_C = (320,)   # channel widths acth_geglu_ffn implements
+
+
+def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p: torch.Tensor,
+              b2: Optional[torch.Tensor], *, residual: Optional[torch.Tensor] = None,
+              mix: Optional[torch.Tensor] = None, mix_alpha: float = 0.0,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused FeedForward(geglu): y = [a*mix + (1-a)*](W2 (h*gelu(g)) + b2 [+ residual]).
+    ``w1``/``b1`` from modules.pack_geglu, ``w2p`` from modules.pack_ffn_w2."""
+    lib = _lib.load()
+    _need(x, torch.bfloat16, "geglu_ffn x")
+    M, C = x.shape
+    if C not in FFN_FUSED_C:
+        raise _lib.ActhError(f"geglu_ffn: C={C} not in {FFN_FUSED_C}")
+    _need(w1, torch.bfloat16, "geglu_ffn w1")
+    _need(w2p, torch.bfloat16, "geglu_ffn w2")
+    if tuple(w1.shape) != (8 * C, C) or tuple(w2p.shape) != (C, 4 * C):
+        raise _lib.ActhError(f"geglu_ffn: weights {tuple(w1.shape)} / {tuple(w2p.shape)} for C={C}")
+    for t, nm in ((b1, "b1"), (b2, "b2")):
+        if t is not None:
+            _need(t, torch.float32, f"geglu_ffn {nm}")
+            if not t.is_contiguous() or t.numel() != (8 * C if nm == "b1" else C):
+                raise _lib.ActhError(f"geglu_ffn {nm}: {tuple(t.shape)}")
+    for t, nm in ((residual, "residual"), (mix, "mix")):
+        if t is not None:
+            _need(t, torch.bfloat16, f"geglu_ffn {nm}")
+            if t.dim() != 2 or t.shape[0] < M or t.shape[1] < C:
+                raise _lib.ActhError(f"geglu_ffn {nm}: {tuple(t.shape)} for ({M}, {C})")
+    if out is None:
+        out = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+    elif out.shape[0] < M or out.shape[1] < C:
+        raise _lib.ActhError(f"geglu_ffn out: {tuple(out.shape)} for ({M}, {C})")
+    d = _lib.FfnDesc()
+    d.x, d.ldx = x.data_ptr(), _rows(x, "geglu_ffn x")
+    d.w1, d.ldw1, d.b1 = w1.data_ptr(), _rows(w1, "geglu_ffn w1"), None if b1 is None else b1.data_ptr()
+    d.w2, d.ldw2, d.b2 = w2p.data_ptr(), _rows(w2p, "geglu_ffn w2"), None if b2 is None else b2.data_ptr()
+    if residual is not None:
+        d.res, d.ldres = residual.data_ptr(), _rows(residual, "geglu_ffn residual")
+    if mix is not None:
+        d.mix, d.ldmix, d.mix_alpha = mix.data_ptr(), _rows(mix, "geglu_ffn mix"), float(mix_alpha)
+    d.y, d.ldy = out.data_ptr(), _rows(out, "geglu_ffn out")
+    d.M, d.C = M, C
+    _lib.check(lib.acth_geglu_ffn(ctypes.byref(d), _stream()), "acth_geglu_ffn")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
 def layernorm(x: torch.Tensor, gamma, beta, eps: float = 1e-5, *, add=None, add_div: int = 1,
               sum_out: Optional[torch.Tensor] = None, out=None):
     lib = _lib.load()

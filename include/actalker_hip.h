@@ -56,6 +56,25 @@ typedef struct ActhGemmDesc {
 int acth_gemm(const ActhGemmDesc* d, hipStream_t stream);
 int acth_gemm_desc_size(void);
 
+/* ---- fused GEGLU feed-forward, C = 320 (FeedForward(activation_fn="geglu") of the level-0
+ * BasicTransformerBlock.ff / TemporalBasicTransformerBlock.ff_in, .ff; attention.py:223-343, 418-473,
+ * activations.py GEGLU): y = [mix_alpha*mix + (1-mix_alpha)*] (W2 (h*gelu(g)) + b2 [+ res]).
+ * w1: (8C, C) bf16 [h|g] rows interleaved in 16-row granules (pack_geglu), b1 likewise (fp32);
+ * w2: 0.5 x (C, 4C) bf16, each 32-column block permuted: column 8q+j <- unit 4q+j (j<4), 16+4q+(j-4). */
+typedef struct ActhFfnDesc {
+  const void* x; int ldx;
+  const void* w1; int ldw1; const float* b1;
+  const void* w2; int ldw2; const float* b2;
+  const void* res; int ldres;
+  const void* mix; int ldmix; float mix_alpha;
+  void* y; int ldy;
+  int M, C;
+} ActhFfnDesc;
+int acth_geglu_ffn(const ActhFfnDesc* d, hipStream_t stream);
+/* diagnostics: host_dst == NULL -> enable (1) / disable (0) per-workgroup phase stamps; else copy the
+ * stamps of the first n_wgs workgroups (8 x u64 s_memtime each) of the last stamped launch */
+int acth_debug_ffn_stamps(unsigned long long* host_dst, int n_wgs, int enable);
+
 /* ---- spatial self-attention, head_dim 64 (AttnProcessor2_0, attention_processor.py:1528-1605) */
 typedef struct ActhAttnDesc {
   const void* q; const void* k; const void* v; void* o;

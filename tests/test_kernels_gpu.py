@@ -94,6 +94,54 @@ def test_gemm_geglu_and_orow(dev):
     assert float(got[0:3].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("M,case", [(1, "res"), (127, "plain"), (300, "res_mix"), (4133, "res"),
+                                    (2 * 128 * 7 + 5, "res_mix"), (640, "nobias")])
+def test_geglu_ffn_fused(dev, M, case):
+    """acth_geglu_ffn (C = 320) against torch fp32 (hidden rounded to bf16 like the kernel) and
+    against the two-GEMM path it replaces."""
+    from actalker_amd.modules import pack_geglu, pack_ffn_w2
+    C, inner = 320, 1280
+    x = bf(rnd(M, C))
+    w1 = rnd(2 * inner, C, scale=C ** -0.5)
+    b1 = rnd(2 * inner, scale=0.1) if case != "nobias" else torch.zeros(2 * inner)
+    w2 = rnd(C, inner, scale=inner ** -0.5)
+    b2 = rnd(C, scale=0.1) if case != "nobias" else None
+    res = bf(rnd(M, C)) if case in ("res", "res_mix") else None
+    mix = bf(rnd(M, C)) if case == "res_mix" else None
+    wp, bp = pack_geglu(w1, b1)
+    w2p = pack_ffn_w2(w2)
+    dv = lambda t: None if t is None else t.to(dev)
+    out = ops.geglu_ffn(x.to(dev), wp.to(dev), None if case == "nobias" else bp.to(dev), w2p.to(dev), dv(b2),
+                        residual=dv(res), mix=dv(mix), mix_alpha=0.3)
+    h, g = (x.float() @ bf(w1).float().t() + b1).chunk(2, -1)
+    hid = bf(h * F.gelu(g)).float()
+    refo = hid @ bf(w2).float().t() + (b2 if b2 is not None else 0.0)
+    if res is not None:
+        refo = refo + res.float()
+    if mix is not None:
+        refo = 0.3 * mix.float() + 0.7 * refo
+    assert out.shape == (M, C)
+    assert rel(out, refo) < 1e-2
+    # the two-kernel path (GEGLU GEMM + output GEMM) on the same packed operands
+    gg = ops.gemm(x.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU)
+    two = ops.gemm(gg, bf(w2).to(dev), bias=dv(b2), residual=dv(res), mix=dv(mix), mix_alpha=0.3)
+    assert rel(out, two) < 4e-3
+
+
+def test_geglu_ffn_rejects_bad_shapes(dev):
+    from actalker_amd import _lib
+    x = torch.zeros(8, 640, device=dev, dtype=torch.bfloat16)
+    w1 = torch.zeros(8 * 640, 640, device=dev, dtype=torch.bfloat16)
+    w2 = torch.zeros(640, 4 * 640, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(_lib.ActhError):
+        ops.geglu_ffn(x, w1, None, w2, None)
+    x = torch.zeros(8, 320, device=dev, dtype=torch.bfloat16)
+    w1 = torch.zeros(8 * 320, 320, device=dev, dtype=torch.bfloat16)
+    w2 = torch.zeros(320, 4 * 320, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(_lib.ActhError):
+        ops.geglu_ffn(x, w1, None, w2, None, residual=torch.zeros(4, 320, device=dev, dtype=torch.bfloat16))
+
+
 @pytest.mark.parametrize("tile", [4, 5])
 @pytest.mark.parametrize("gm", [1, 3, 8])
 def test_gemm_grouped_raster(dev, tile, gm):

@@ -4,6 +4,7 @@ per-dispatch counters then belong to a single kernel configuration.
   python tools/pmc_probe.py gemm <SHAPES index> [--residual]
   python tools/pmc_probe.py flash <nbatch> <S> <heads>
   python tools/pmc_probe.py scan <nb> <L> <D> <R>
+  python tools/pmc_probe.py ffn <M>
 """
 import argparse
 import os
@@ -45,6 +46,18 @@ def main():
         Dp = torch.ones(2 * D).to(dev)
         for _ in range(a.iters):
             ops.selective_scan(u, xdbl, dtw, dtb, alog, Dp, nb=nb, L=L, R=R, n_keep=L - 33)
+        torch.cuda.synchronize()
+    elif a.kind == "ffn":
+        from actalker_amd.modules import pack_ffn_w2, pack_geglu
+        M, C = a.args[0], 320
+        x = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
+        res = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
+        w1, b1 = pack_geglu(torch.randn(8 * C, C, generator=g) * C ** -0.5, 0.1 * torch.randn(8 * C, generator=g))
+        w2 = pack_ffn_w2(torch.randn(C, 4 * C, generator=g) * (4 * C) ** -0.5)
+        w1, b1, w2 = w1.to(dev), b1.to(dev), w2.to(dev)
+        b2 = torch.zeros(C, device=dev)
+        for _ in range(a.iters):
+            ops.geglu_ffn(x, w1, b1, w2, b2, residual=res)
         torch.cuda.synchronize()
     else:
         raise SystemExit(f"unknown kind {a.kind}")

@@ -5,26 +5,30 @@
 //     [h | g] = W1 x + b1,  W1: (2I, C), W2: (C, I), I = 4C.
 // Two GEMMs and a 4C-wide hidden tensor per token become one kernel whose hidden activations never
 // reach HBM -- the structure of flash attention (S = K Q^T -> P -> O += V^T P^T):
-//   * a workgroup owns 128 tokens: 4 wave pairs x 32 tokens (two 16-token groups). A wave's 32
-//     token rows of x live in VGPRs for the whole kernel as the up projection's B operand;
-//   * the hidden dimension is walked in chunks of 32 gated units (64 rows of W1 = two 16-row
-//     (hidden | gate) granules of modules.pack_geglu; 32 columns of W2), double-buffered in LDS by
-//     LDS-DMA. Wave `half` of a pair computes granule `half` of the chunk for the pair's 32 tokens,
-//     H^T = W1g x^T (v_mfma_f32_16x16x32_bf16; every W1 fragment read feeds two MFMAs), gates it in
-//     registers (lane (t, q) holds units 4q..4q+3 of both the hidden and the gate fragment) and
-//     swaps the 4 gated units per token with its partner through LDS; then it accumulates output
-//     channels [160*half, +160) of O^T += W2c H^T for the 32 tokens. A lane's 4 + 4 units are the
-//     down projection's B operand directly, W2's K order permuted to match at pack time (within each
-//     32-column block, column 8q + j <- unit 4q + j (j < 4) or 16 + 4q + (j - 4)) and scaled by 0.5;
-//   * software pipeline, one barrier per chunk: iteration c runs up(c), down(c-1), gate(c), so the
-//     gate VALU has independent MFMAs to overlap; W1(c+1) and W2(c) are in flight meanwhile;
+//   * a workgroup owns 128 tokens: 4 wave pairs x 32 tokens. A wave's 32 token rows of x live in
+//     VGPRs for the whole kernel as the up projection's B operand (v_mfma_f32_32x32x16_bf16: 32x32
+//     fragments hold the MFMA shadow at 8 of 32 issue cycles, against 8 of 16 for 16x16x32);
+//   * the hidden dimension is walked in chunks of 32 gated units (64 rows of W1 = two 32-row
+//     [hidden 16 | gate 16] granules of modules.pack_geglu; 32 columns of W2), double-buffered in
+//     LDS by LDS-DMA. Wave `half` of a pair computes granule `half` for the pair's 32 tokens,
+//     H^T = W1g x^T (one 32x32 fragment: lane (t, hi) holds hidden rows 8 jb + 4 hi + r and the gate
+//     rows 16 higher, so the gate is lane-local), gates it in registers, keeps its 8 gated units and
+//     swaps them with its partner through LDS; then it accumulates output channels
+//     [C/2 * half, +C/2) of O^T += W2c H^T for the 32 tokens. A lane's 8 units are the down
+//     projection's B operand as they stand: W2's K order is permuted at pack time to match (within
+//     each 16-unit granule, column 8 hi + e <- unit 8 (e / 4) + 4 hi + e % 4) and scaled by 0.5;
+//   * software pipeline, one barrier per chunk: iteration c runs up(c), then down(c-1) with gate(c)
+//     interleaved into its MFMA slots; W1(c+1) and W2(c) are in flight meanwhile. Measured (in-kernel
+//     stamps, tools/ffn_stamps.py): the LDS-DMA issue of the 60 KB weight chunk (~65 cycles per 1 KB
+//     piece) is the largest cost after the MFMAs -- the price of 128 tokens per weight pass, which is
+//     what the VGPR (x rows, O^T accumulators) and LDS (double-buffered chunks) budgets allow;
 //   * epilogue: O^T fragments -> per-wave LDS slab (token-major) -> + b2, residual, mix -> 16-byte
 //     row stores.
 // Numerics match the two-kernel path: fp32 accumulation, the gated hidden rounded to bf16 before the
 // down projection (as the GEGLU GEMM's bf16 output was); GELU by the degree-8 erf fit below.
-// LDS images (conflict-free ds_read_b128 for the gfx950 lane groups): W1 chunk 64 rows x C/8 16-byte
-// chunks, chunk index XOR (row & 7) inside 8-chunk groups; W2 chunk C rows x 4 chunks, chunk index
-// XOR ((row >> 1) & 2).
+// LDS images (conflict-free ds_read_b128 of 32-row fragments for the gfx950 lane groups): W1 chunk
+// 64 rows x C/8 16-byte chunks, chunk index XOR ((row >> 1) & 7) inside 8-chunk groups; W2 chunk C
+// rows x 4 chunks, chunk index XOR ((row >> 2) & 3).
 #include <type_traits>
 
 #include "common.h"
@@ -69,18 +73,19 @@ template <int C>
 __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, unsigned w1_bytes,
                                                            unsigned w2_bytes) {
   constexpr int I = 4 * C;                // hidden units
-  constexpr int KS = C / 32;              // k steps of the up projection
-  constexpr int HF = C / 32;              // output fragments (16 channels) per wave: half of C / 16
-  constexpr int HC = 32;                  // gated units per chunk
+  constexpr int KS = C / 16;              // k steps (16) of the up projection
+  constexpr int HF = C / 64;              // output fragments (32 channels) per wave: half of C / 32
+  constexpr int HC = 32;                  // gated units per chunk (two 16-unit granules)
   constexpr int NCH = I / HC;             // chunks
   constexpr int W1R = 2 * HC;             // W1 rows per chunk
   constexpr int W1CH = C / 8;             // 16-byte chunks per W1 row
   constexpr int W1B = W1R * C * 2;        // bytes of a W1 chunk image
   constexpr int W2B = C * HC * 2;         // bytes of a W2 chunk image (C rows x 64 B)
-  constexpr int HXB = 8 * 2 * 64 * 8;     // gated-unit exchange: [pair 4][tg 2][half 2][lane 64] x 8 B
+  constexpr int HXB = 4 * 2 * 64 * 16;    // gated-unit exchange: [pair 4][half 2][lane 64] x 16 B
   constexpr int NI1 = W1B / 1024, NI2 = W2B / 1024;   // DMA wave-instructions per chunk
   constexpr int NI1W = (NI1 + 7) / 8, NI2W = (NI2 + 7) / 8;
-  static_assert(C % 32 == 0 && HF % 2 == 0 && W1CH % 8 == 0 && W1B % 1024 == 0 && W2B % 1024 == 0, "shape");
+  constexpr int NS = KS + 2 * HF;         // MFMA slots per chunk iteration
+  static_assert(C % 64 == 0 && W1CH % 8 == 0 && W1B % 1024 == 0 && W2B % 1024 == 0 && KS % 4 == 0, "shape");
   static_assert(2 * (W1B + W2B + HXB) + (2 * I + C) * 4 <= 160 * 1024, "LDS");
   // Every buffer is its own LDS object and the chunk loop is unrolled by two so each access names
   // its buffer at compile time: the compiler then knows an LDS-DMA write into one buffer never
@@ -96,28 +101,31 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
     if (stamps && tid == 0) g_ffn_stamps[blockIdx.x * FFN_NSTAMP + k] = __builtin_amdgcn_s_memtime();
   };
   stamp(0);
-  const int t16 = lane & 15, q = lane >> 4;
+  const int l32 = lane & 31, hi = lane >> 5;
   const int tok0 = blockIdx.x * 128 + pr * 32;             // the pair's first token
+  const int tok = tok0 + l32;                              // this lane's token (B-operand column)
 
   const __amdgpu_buffer_rsrc_t r1 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.w1), (short)0, (int)w1_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t r2 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.w2), (short)0, (int)w2_bytes, 0x00020000);
 
-  // ---- DMA source offsets of this lane's 16-byte chunk of each image instruction
+  // ---- DMA source offsets of this lane's 16-byte chunk of each image instruction. W1 image: 64 rows
+  // x W1CH chunks, chunk index XOR ((row >> 1) & 7) inside 8-chunk groups; W2 image: C rows x 4
+  // chunks, chunk index XOR ((row >> 2) & 3) -- conflict-free ds_read_b128 of 32-row fragments.
   unsigned o1[NI1W], o2[NI2W];
 #pragma unroll
   for (int u = 0; u < NI1W; ++u) {
     const int pc = (wave + 8 * u) * 64 + lane;
     const int row = pc / W1CH, pch = pc - row * W1CH;
-    const int lch = (pch & ~7) | ((pch ^ row) & 7);
+    const int lch = (pch & ~7) | ((pch ^ (row >> 1)) & 7);
     o1[u] = ((unsigned)row * p.ldw1 + lch * 8) * 2u;
   }
 #pragma unroll
   for (int u = 0; u < NI2W; ++u) {
     const int pc = (wave + 8 * u) * 64 + lane;
     const int row = pc >> 2, pch = pc & 3;
-    const int lch = pch ^ ((row >> 1) & 2);
+    const int lch = pch ^ ((row >> 2) & 3);
     o2[u] = ((unsigned)row * p.ldw2 + lch * 8) * 2u;
   }
   auto stage_w1 = [&](int ch, auto par) {
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
 #pragma unroll
     for (int u = 0; u < NI1W; ++u)
       if (NI1 % 8 == 0 || wave + 8 * u < NI1)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_void*)(d + (wave + 8 * u) * 1024), 16, (int)(o1[u] + b), 0,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_void*)(d + (wave + 8 * u) * 1024), 16, (int)o1[u], (int)b,
                                                  0, 0);
   };
   auto stage_w2 = [&](int ch, auto par) {
@@ -135,21 +143,20 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
 #pragma unroll
     for (int u = 0; u < NI2W; ++u)
       if (NI2 % 8 == 0 || wave + 8 * u < NI2)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_void*)(d + (wave + 8 * u) * 1024), 16, (int)(o2[u] + b), 0,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_void*)(d + (wave + 8 * u) * 1024), 16, (int)o2[u], (int)b,
                                                  0, 0);
   };
 
-  // ---- the pair's 2 x 16 token rows of x, as the up projection's B operand for every k step
-  bf16x8_t xf[2][KS];
-#pragma unroll
-  for (int tg = 0; tg < 2; ++tg) {
-    const int tok = tok0 + tg * 16 + t16;
-    const bf16_t* xr = (const bf16_t*)p.x + (size_t)(tok < p.M ? tok : 0) * p.ldx + 8 * q;
+  // ---- this lane's token row of x as the up projection's B operand: k step ks holds channels
+  // 16 ks + 8 hi .. + 7
+  bf16x8_t xf[KS];
+  {
+    const bf16_t* xr = (const bf16_t*)p.x + (size_t)(tok < p.M ? tok : 0) * p.ldx + 8 * hi;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      uint4 v = *reinterpret_cast<const uint4*>(xr + 32 * ks);
+      uint4 v = *reinterpret_cast<const uint4*>(xr + 16 * ks);
       if (tok >= p.M) v = make_uint4(0, 0, 0, 0);
-      xf[tg][ks] = __builtin_bit_cast(bf16x8_t, v);
+      xf[ks] = __builtin_bit_cast(bf16x8_t, v);
     }
   }
   for (int i = tid; i < 2 * I; i += 512) sb1[i] = p.b1 ? p.b1[i] : 0.0f;
@@ -159,103 +166,91 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
   __syncthreads();
   stamp(1);
 
-  f32x4_t acc[2][HF];
+  // O^T accumulators: fragment f holds channels half*C/2 + 32 f + 8 jb + 4 hi + r (register 4 jb + r)
+  // of token tok0 + l32
+  f32x16_t acc[HF];
 #pragma unroll
-  for (int tg = 0; tg < 2; ++tg)
+  for (int f = 0; f < HF; ++f)
 #pragma unroll
-    for (int f = 0; f < HF; ++f) acc[tg][f] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int e = 0; e < 16; ++e) acc[f][e] = 0.0f;
 
-  // fragment-read lane offsets. W1 image: row half*32 + 16 i + t16, logical chunk 4 s + q stored at
-  // (4 s & ~7) | ((4 s + q) ^ row) & 7 = 8 (s >> 1) + (4 (s & 1) ^ key), key = q ^ (t16 & 7).
-  // W2 image: row half*C/2 + 16 f + t16, chunk q ^ ((t16 >> 1) & 2).
-  const int key = q ^ (t16 & 7);
-  const int a1e = (half * 32 + t16) * (W1CH * 16) + key * 16;
-  const int a1o = (half * 32 + t16) * (W1CH * 16) + (4 ^ key) * 16;
-  const int a2 = (half * (C / 2) + t16) * 64 + (q ^ ((t16 >> 1) & 2)) * 16;
-  const int hx_w = ((pr * 2) * 2 + half) * 512 + lane * 8;   // + tg * 1024: this wave's exchange slot
-  const int hx_r = (pr * 2) * 2 * 512 + lane * 8;            // + tg * 1024 + partner * 512
+  // fragment-read lane offsets. W1: row half*32 + l32 (its (row >> 1) & 7 is (l32 >> 1) & 7), logical
+  // chunk 2 ks + hi stored at 8 (ks >> 2) + ((2 (ks & 3) + hi) ^ key1): four per-lane offsets by ks & 3.
+  const int key1 = (l32 >> 1) & 7, key2 = (l32 >> 2) & 3;
+  int a1[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) a1[m] = (half * 32 + l32) * (W1CH * 16) + (((2 * m + hi) ^ key1) * 16);
+  // W2: row half*C/2 + 32 f + l32, chunk 2 G + hi (granule G) XOR key2; own granule first
+  const int a2own = (half * (C / 2) + l32) * 64 + (((2 * half + hi) ^ key2) * 16);
+  const int a2par = (half * (C / 2) + l32) * 64 + (((2 * (half ^ 1) + hi) ^ key2) * 16);
+  const int hx_w = (pr * 2 + half) * 1024 + lane * 16;
+  const int hx_r = (pr * 2 + (half ^ 1)) * 1024 + lane * 16;
 
-  // one chunk iteration: up(c) [UP], down(c-1) [DN], gate(c) [UP]. The fragment reads run 3 slots
-  // ahead of their MFMAs (a slot = one up k step, 4 MFMAs, or one down fragment, 2 MFMAs) and
-  // sched_barriers pin that order, so LDS latency hides under the MFMAs of the slots between.
+  bf16x8_t hown;                                           // this wave's gated units of the last chunk
+  // one chunk iteration: up(c) [UP]; down(c-1) [DN] with gate(c) [UP] interleaved into its slots
+  // (independent work: the gate's VALU issues in the MFMA shadow). Fragment reads run 3 slots ahead
+  // of their MFMAs; sched_barriers pin the order.
   auto body = [&](int c, auto up_c, auto dn_c, auto par_c) {
     constexpr bool UP = decltype(up_c)::value, DN = decltype(dn_c)::value, PAR = decltype(par_c)::value;
-    constexpr int NS = KS + HF;
     using Par = std::integral_constant<bool, PAR>;
     using NPar = std::integral_constant<bool, !PAR>;
     if (UP && c + 1 < NCH) stage_w1(c + 1, NPar{});
     if (UP) stage_w2(c, Par{});
     const char* s1 = PAR ? w1s1 : w1s0;
     const char* s2 = PAR ? w2s0 : w2s1;                      // W2 of chunk c - 1
-    const char* hxr = (PAR ? hxs0 : hxs1) + hx_r;
-    f32x4_t u[2][2];
+    const char* hxr = (PAR ? hxs0 : hxs1) + hx_r;           // partner's units of chunk c - 1
+    char* hxw = (PAR ? hxs1 : hxs0) + hx_w;
+    f32x16_t u;
     if constexpr (UP) {
-      const float* bb = sb1 + c * W1R + half * 32 + 4 * q;
-      const f32x4_t bh = *reinterpret_cast<const f32x4_t*>(bb);
-      const f32x4_t bg = *reinterpret_cast<const f32x4_t*>(bb + 16);
-      u[0][0] = u[1][0] = bh;
-      u[0][1] = u[1][1] = bg;
+      const float* bb = sb1 + c * W1R + half * 32 + 4 * hi;
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bb + 8 * jb);
+        u[4 * jb] = b4.x; u[4 * jb + 1] = b4.y; u[4 * jb + 2] = b4.z; u[4 * jb + 3] = b4.w;
+      }
     }
-    bf16x8_t fr[4][2], hb[2];
+    bf16x8_t fr[4], hpar;
+    float sg[8];
     auto load = [&](auto s_c) {
       constexpr int s = decltype(s_c)::value;
       if constexpr (s < KS) {
-        if constexpr (UP) {
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            fr[s & 3][i] = *reinterpret_cast<const bf16x8_t*>(s1 + ((s & 1) ? a1o : a1e) + i * 16 * (W1CH * 16) +
-                                                              (s >> 1) * 128);
-        }
+        if constexpr (UP) fr[s & 3] = *reinterpret_cast<const bf16x8_t*>(s1 + a1[s & 3] + (s >> 2) * 128);
       } else if constexpr (s < NS) {
         if constexpr (DN) {
-          fr[s & 3][0] = *reinterpret_cast<const bf16x8_t*>(s2 + a2 + (s - KS) * 1024);
+          constexpr int f = (s - KS) >> 1, own = ((s - KS) & 1) == 0;
+          fr[s & 3] = *reinterpret_cast<const bf16x8_t*>(s2 + (own ? a2own : a2par) + f * 32 * 64);
         }
       }
+    };
+    auto gate = [&](int e) {                                 // unit 8 (e / 4) + 4 hi + e % 4 of the granule
+      const float h = u[(e >> 2) * 4 + (e & 3)], g = u[8 + (e >> 2) * 4 + (e & 3)], hg = h * g;
+      sg[e] = fmaf(hg, erf_scaled(g), hg);
     };
     static_for<0, 3>(load);
     static_for<0, NS>([&](auto s_c) {
       constexpr int s = decltype(s_c)::value;
       load(std::integral_constant<int, s + 3>{});
-      if constexpr (DN && s == (KS >= 4 ? KS - 4 : 0)) {
-#pragma unroll
-        for (int tg = 0; tg < 2; ++tg) {
-          const uint2 lo = *reinterpret_cast<const uint2*>(hxr + tg * 1024);
-          const uint2 hi = *reinterpret_cast<const uint2*>(hxr + tg * 1024 + 512);
-          hb[tg] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
-        }
-      }
+      if constexpr (DN && s == KS - 6) hpar = *reinterpret_cast<const bf16x8_t*>(hxr);
       if constexpr (s < KS) {
-        if constexpr (UP) {
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            u[0][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s & 3][i], xf[0][s], u[0][i], 0, 0, 0);
-            u[1][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s & 3][i], xf[1][s], u[1][i], 0, 0, 0);
-          }
-        }
+        if constexpr (UP) u = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s & 3], xf[s], u, 0, 0, 0);
       } else {
         if constexpr (DN) {
-          constexpr int f = s - KS;
-          acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s & 3][0], hb[0], acc[0][f], 0, 0, 0);
-          acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[s & 3][0], hb[1], acc[1][f], 0, 0, 0);
+          constexpr int f = (s - KS) >> 1, own = ((s - KS) & 1) == 0;
+          acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s & 3], own ? hown : hpar, acc[f], 0, 0, 0);
         }
+        if constexpr (UP && DN && s >= KS + 1 && s < KS + 9) gate(s - KS - 1);
       }
       __builtin_amdgcn_sched_barrier(0);
     });
     if constexpr (UP) {
-      // GEGLU gate of granule `half` (b1 entered as the accumulators' initial value); lane (t, q) holds
-      // units 4q + r of its token in each group. Stored: 2 h gelu(g) = h g (1 + erf(g / sqrt 2)),
-      // the factor 2 undone by W2's pack-time 0.5 (exact: both are powers of two).
-      char* hx = (PAR ? hxs1 : hxs0) + hx_w;
+      if constexpr (!DN) {
 #pragma unroll
-      for (int tg = 0; tg < 2; ++tg) {
-        float s4[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = u[tg][1][r], hg = u[tg][0][r] * g;
-          s4[r] = fmaf(hg, erf_scaled(g), hg);
-        }
-        *reinterpret_cast<uint2*>(hx + tg * 1024) = make_uint2(pack2(s4[0], s4[1]), pack2(s4[2], s4[3]));
+        for (int e = 0; e < 8; ++e) gate(e);
       }
+      // stored: 2 h gelu(g) = h g (1 + erf(g / sqrt 2)), the factor 2 undone by W2's pack-time 0.5
+      hown = __builtin_bit_cast(bf16x8_t, make_uint4(pack2(sg[0], sg[1]), pack2(sg[2], sg[3]),
+                                                     pack2(sg[4], sg[5]), pack2(sg[6], sg[7])));
+      *reinterpret_cast<bf16x8_t*>(hxw) = hown;
     }
     // W1(c+1), W2(c) landed, gated units of chunk c visible, everyone done with the buffers the
     // next iteration re-stages
@@ -275,37 +270,44 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
   body(NCH, std::false_type{}, std::true_type{}, std::false_type{});
   stamp(5);
 
-  // ---- epilogue per token group: O^T -> per-wave fp32 slab [16 tokens][C/2 + 4] -> token rows of
-  // 8-channel chunks (+ b2, residual, AlphaBlender mix) -> 16-byte stores
-  constexpr int HALF = C / 2, LD = HALF, CPR = HALF / 8, NCK = 16 * CPR / 64;
-  static_assert(4 * 16 * LD * 4 <= W1B && 16 * CPR % 64 == 0 && (HALF / 4) % 8 == 0, "epilogue slab");
-  float* const sl = reinterpret_cast<float*>(wave < 4 ? w1s0 : w1s1) + (wave & 3) * (16 * LD);
-  // 16-byte column chunk k of slab row r lives at chunk (k & ~7) | ((k ^ r) & 7): conflict-free
-  auto slab = [&](int r, int k) { return &sl[r * LD + (((k & ~7) | ((k ^ r) & 7)) << 2)]; };
-#pragma unroll
-  for (int tg = 0; tg < 2; ++tg) {
-    const int trow0 = tok0 + tg * 16;
+  // ---- epilogue in passes of up to two fragments (64 channels): O^T -> per-wave fp32 slab
+  // [32 tokens][64] (16-byte chunk index XOR (row & 7)) -> token rows of 8-channel chunks (+ b2,
+  // residual, AlphaBlender mix) -> 16-byte stores
+  constexpr int LD = 64;
+  static_assert(4 * 32 * LD * 4 <= W1B, "epilogue slab");
+  float* const sl = reinterpret_cast<float*>(wave < 4 ? w1s0 : w1s1) + (wave & 3) * (32 * LD);
+  auto slab = [&](int r, int k) { return &sl[r * LD + ((k ^ (r & 7)) << 2)]; };
+  static_for<0, (HF + 1) / 2>([&](auto p_c) {
+    constexpr int P = decltype(p_c)::value;
+    constexpr int NFP = (2 * P + 1 < HF) ? 2 : 1;           // fragments in this pass
+    constexpr int CPT = NFP * 4;                              // 8-channel chunks per token row
+    constexpr int NCK = 32 * CPT / 64;                        // chunks per lane
+    const int ch0 = half * (C / 2) + P * 64;
     uint4 rr[NCK], mm[NCK];
 #pragma unroll
     for (int k = 0; k < NCK; ++k) {
-      const int ck = lane + 64 * k, tr = ck / CPR, c8 = (ck - tr * CPR) * 8;
-      const int tk = trow0 + tr < p.M ? trow0 + tr : 0;
-      const int col = half * HALF + c8;
-      rr[k] = p.res ? *reinterpret_cast<const uint4*>((const bf16_t*)p.res + (size_t)tk * p.ldres + col)
+      const int ck = lane + 64 * k, tr = ck / CPT, c8 = (ck - tr * CPT) * 8;
+      const int tk = tok0 + tr < p.M ? tok0 + tr : 0;
+      rr[k] = p.res ? *reinterpret_cast<const uint4*>((const bf16_t*)p.res + (size_t)tk * p.ldres + ch0 + c8)
                     : make_uint4(0, 0, 0, 0);
-      mm[k] = p.mix ? *reinterpret_cast<const uint4*>((const bf16_t*)p.mix + (size_t)tk * p.ldmix + col)
+      mm[k] = p.mix ? *reinterpret_cast<const uint4*>((const bf16_t*)p.mix + (size_t)tk * p.ldmix + ch0 + c8)
                     : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int f = 0; f < HF; ++f)
-      *reinterpret_cast<f32x4_t*>(slab(t16, f * 4 + q)) = acc[tg][f];
+    for (int f = 0; f < NFP; ++f)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const f32x16_t& a = acc[2 * P + f];
+        *reinterpret_cast<f32x4_t*>(slab(l32, f * 8 + 2 * jb + hi)) =
+            f32x4_t{a[4 * jb], a[4 * jb + 1], a[4 * jb + 2], a[4 * jb + 3]};
+      }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < NCK; ++k) {
-      const int ck = lane + 64 * k, tr = ck / CPR, c8 = (ck - tr * CPR) * 8;
+      const int ck = lane + 64 * k, tr = ck / CPT, c8 = (ck - tr * CPT) * 8;
       const float4 x0 = *reinterpret_cast<const float4*>(slab(tr, c8 / 4));
       const float4 x1 = *reinterpret_cast<const float4*>(slab(tr, c8 / 4 + 1));
-      const int col = half * HALF + c8;
+      const int col = ch0 + c8;
       const float4 b0 = *reinterpret_cast<const float4*>(&sb2[col]);
       const float4 b1 = *reinterpret_cast<const float4*>(&sb2[col + 4]);
       float v[8] = {x0.x + b0.x, x0.y + b0.y, x0.z + b0.z, x0.w + b0.w,
@@ -322,11 +324,10 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = p.mix_alpha * t[e] + (1.0f - p.mix_alpha) * v[e];
       }
-      if (trow0 + tr < p.M)
-        *reinterpret_cast<uint4*>((bf16_t*)p.y + (size_t)(trow0 + tr) * p.ldy + col) = pack8(v);
+      if (tok0 + tr < p.M) *reinterpret_cast<uint4*>((bf16_t*)p.y + (size_t)(tok0 + tr) * p.ldy + col) = pack8(v);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slab reads done before the next group's writes
-  }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     // slab reads done before the next pass's writes
+  });
   stamp(6);
 }
 

@@ -388,11 +388,71 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
       }
       float y = y2.x + y2.y;
       y += pair_swap(y);
-      if (half == 0) ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uu, y));
+      // both lanes of the pair hold the same y and store the same bf16: an unconditional store keeps
+      // the unrolled tile one basic block, so the scheduler can overlap the h-independent work
+      // (dt, softplus, exps) of later tokens with the serial state updates
+      ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uu, y));
     };
     if (nt == SC_T) {
+      // Full tile, software-pipelined by hand (the compiler schedules each token's dependency chain
+      // on its own): (1) dt = softplus(dt_proj) and u of all SC_T tokens -- independent of the state;
+      // (2) the recurrence, with token tt+1's decays exp(dt A) and inputs dt u B computed before
+      // token tt's state update so their latency hides under it.
+      float dtv[SC_T], uuv[SC_T];
 #pragma unroll
-      for (int tt = 0; tt < SC_T; ++tt) token(tt);
+      for (int tt = 0; tt < SC_T; ++tt) {
+        const float* xr = xs + tt * WP;
+        float dt;
+        if constexpr (R == 0) {
+          dt = dls[tt * SP_CH + cl] + bias;
+        } else {
+          const float4* xr4 = reinterpret_cast<const float4*>(xr + half * R0P);
+          f32x2_t part = {0.0f, 0.0f};
+#pragma unroll
+          for (int r4 = 0; r4 < R0P / 4; ++r4) {
+            const float4 v = xr4[r4];
+            part = __builtin_elementwise_fma(w2[2 * r4], (f32x2_t){v.x, v.y}, part);
+            part = __builtin_elementwise_fma(w2[2 * r4 + 1], (f32x2_t){v.z, v.w}, part);
+          }
+          const float ph = part.x + part.y;
+          dt = ph + pair_swap(ph) + bias;
+        }
+        dtv[tt] = SOFTPLUS ? softplus_raw(dt) : dt;
+        uuv[tt] = bf2f(us[tt * SP_CH + cl]);
+      }
+      f32x2_t ee[2][4], db[2][4];
+      auto prep = [&](int tt, int slot) {
+        const float* xr = xs + tt * WP;
+        const float4* bv = reinterpret_cast<const float4*>(xr + 2 * R0P + 8 * half);
+        const float4 b0 = bv[0], b1 = bv[1];
+        const f32x2_t bb[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
+        const float dt = dtv[tt], du = dt * uuv[tt];
+        const f32x2_t dt2 = {dt, dt}, du2 = {du, du};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const f32x2_t x = dt2 * a2[n];
+          ee[slot][n] = (f32x2_t){fast_exp2(x.x), fast_exp2(x.y)};
+          db[slot][n] = du2 * bb[n];
+        }
+      };
+      prep(0, 0);
+#pragma unroll
+      for (int tt = 0; tt < SC_T; ++tt) {
+        if (tt + 1 < SC_T) prep(tt + 1, (tt + 1) & 1);
+        const float* xr = xs + tt * WP;
+        const float4* cv = reinterpret_cast<const float4*>(xr + 2 * R0P + 16 + 8 * half);
+        const float4 c0 = cv[0], c1 = cv[1];
+        const f32x2_t cc[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
+        f32x2_t y2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          h[n] = __builtin_elementwise_fma(ee[tt & 1][n], h[n], db[tt & 1][n]);
+          y2 = __builtin_elementwise_fma(h[n], cc[n], y2);
+        }
+        float y = y2.x + y2.y;
+        y += pair_swap(y);
+        ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uuv[tt], y));
+      }
     } else {
       for (int tt = 0; tt < nt; ++tt) token(tt);
     }

@@ -86,12 +86,12 @@ def pack_geglu(w: torch.Tensor, b: torch.Tensor):
 
 
 def ffn_w2_perm(inner: int) -> torch.Tensor:
-    """Column order of the fused feed-forward's W2 (acth_geglu_ffn): within each 32-unit hidden chunk,
-    column 8q + j holds unit 4q + j (j < 4) or 16 + 4q + (j - 4) -- the order in which a lane of the
-    up-projection's 16x16 MFMA fragments holds the gated units (rows 4q..4q+3 of the two granules)."""
-    q, j = torch.arange(4).view(4, 1), torch.arange(8).view(1, 8)
-    local = torch.where(j < 4, 4 * q + j, 16 + 4 * q + (j - 4)).reshape(32)
-    return (torch.arange(0, inner, 32).view(-1, 1) + local.view(1, 32)).reshape(-1)
+    """Column order of the fused feed-forward's W2 (acth_geglu_ffn): within each 16-unit granule, column
+    8 hi + e holds unit 8 (e // 4) + 4 hi + e % 4 -- the order in which lane (token, hi) of the
+    up projection's 32x32 MFMA fragment holds its 8 gated units, i.e. the down projection's K order."""
+    hi, e = torch.arange(2).view(2, 1), torch.arange(8).view(1, 8)
+    local = (8 * (e // 4) + 4 * hi + e % 4).reshape(16)
+    return (torch.arange(0, inner, 16).view(-1, 1) + local.view(1, 16)).reshape(-1)
 
 
 def pack_ffn_w2(w: torch.Tensor) -> torch.Tensor:

@@ -187,7 +187,7 @@ class GemmTimer:
 class FamilyTimer:
     """HIP events around every launch of the non-GEMM kernel families on the launch stream inside the
     timed region, with each launch's algorithmic work: flash attention FLOPs (4 S^2 64 per head and
-    batch), selective-scan bytes (u read once for both directions, the fp32 xdbl rows, both outputs
+    batch), fused level-0 feed-forward FLOPs (24 M C^2), selective-scan bytes (u read once for both directions, the fp32 xdbl rows, both outputs
     written), GroupNorm / LayerNorm bytes (input read once, output written once -- the stats pass's
     second read of the input is the kernels' cost, not the algorithm's)."""
 
@@ -227,7 +227,12 @@ class FamilyTimer:
         def w_ln(x, *a, add=None, sum_out=None, **k):
             return 2.0 * x.numel() * 2 + (x.numel() * 2 if sum_out is not None else 0)
 
+        def w_ffn(x, *a, **k):
+            M, C = x.shape
+            return 24.0 * M * C * C                  # up 2*M*C*8C + down 2*M*4C*C
+
         self._wrap(ops, "flash_attn", "flash_attn", w_flash)
+        self._wrap(ops, "geglu_ffn", "geglu_ffn", w_ffn)
         self._wrap(ops, "selective_scan", "selective_scan", w_scan)
         self._wrap(ops, "groupnorm", "groupnorm", w_gn)
         self._wrap(ops, "layernorm", "layernorm", w_ln)
@@ -240,6 +245,7 @@ class FamilyTimer:
 
     def report(self, step_ms_total):
         peak = {"flash_attn": ("mfma", PEAK_BF16_TFLOPS, "TFLOP/s", 1e12),
+                "geglu_ffn": ("mfma", PEAK_BF16_TFLOPS, "TFLOP/s", 1e12),
                 "selective_scan": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
                 "groupnorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
                 "layernorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9)}

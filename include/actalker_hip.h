@@ -60,7 +60,7 @@ int acth_gemm_desc_size(void);
  * BasicTransformerBlock.ff / TemporalBasicTransformerBlock.ff_in, .ff; attention.py:223-343, 418-473,
  * activations.py GEGLU): y = [mix_alpha*mix + (1-mix_alpha)*] (W2 (h*gelu(g)) + b2 [+ res]).
  * w1: (8C, C) bf16 [h|g] rows interleaved in 16-row granules (pack_geglu), b1 likewise (fp32);
- * w2: 0.5 x (C, 4C) bf16, each 32-column block permuted: column 8q+j <- unit 4q+j (j<4), 16+4q+(j-4). */
+ * w2: 0.5 x (C, 4C) bf16, each 16-column block permuted: column 8hi+e <- unit 8(e/4)+4hi+e%4 (modules.ffn_w2_perm). */
 typedef struct ActhFfnDesc {
   const void* x; int ldx;
   const void* w1; int ldw1; const float* b1;

@@ -203,6 +203,49 @@ static int choose_tile(const ActhGemmDesc* d) {
   return 3;
 }
 
+// An A operand past the kernels' 2 GiB buffer extent (32-bit buffer offsets / num_records) runs as
+// consecutive launches over row chunks whose A extents fit, the descriptor rebased per chunk: rows
+// of C / R / MIX and row-bias images shifted, A (and A2) advanced by the chunk's first source row.
+// A chunk is whole units of the A mode -- any rows (dense), whole images (conv: the 3x3 taps stay
+// inside an image), whole batch elements (temporal: the frame taps stay inside one) -- and whole
+// row-bias images. Row remaps (rmap, orow) are not rebased: such calls keep the 2 GiB limit.
+// (The 112-frame mode-2 UNet call at 576x1024 reads 2.7 GB Mamba xz rows through x_proj.)
+extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream);
+
+static int gemm_split_rows(const ActhGemmDesc* d, hipStream_t stream) {
+  if (d->rmap || d->orow_div < d->M) return ACTH_EINVAL;
+  long long unit_rows = 1, unit_arows = 1;                 // output rows / A rows per indivisible unit
+  if (d->amode == 1) { unit_rows = (long long)d->Ho * d->Wo; unit_arows = (long long)d->H * d->W; }
+  if (d->amode == 2) { unit_rows = unit_arows = (long long)d->F * d->S; }
+  if (d->rowbias) {
+    long long g = unit_rows, r = d->rb_div;                // unit := lcm(unit, rb_div) output rows
+    while (r) { const long long t = g % r; g = r; r = t; }
+    const long long mult = d->rb_div / g;
+    unit_rows *= mult; unit_arows *= mult;
+  }
+  if (d->M % unit_rows && d->amode != 0) return ACTH_EINVAL;
+  const long long lda_max = d->A2 ? (d->lda > d->lda2 ? d->lda : d->lda2) : d->lda;
+  const long long units_per_chunk = ((0x7fffffffLL / 2) - 65536) / (unit_arows * lda_max);
+  if (units_per_chunk < 1) return ACTH_EINVAL;
+  const long long chunk_rows = units_per_chunk * unit_rows, chunk_arows = units_per_chunk * unit_arows;
+  const int esz = d->out_f32 ? 4 : 2;
+  for (long long m0 = 0, a0 = 0; m0 < d->M; m0 += chunk_rows, a0 += chunk_arows) {
+    ActhGemmDesc c = *d;
+    const long long mc = (d->M - m0 < chunk_rows) ? d->M - m0 : chunk_rows;
+    c.M = (int)mc;
+    c.A = (const char*)d->A + a0 * d->lda * 2;
+    if (d->A2) c.A2 = (const char*)d->A2 + a0 * d->lda2 * 2;
+    c.C = (char*)d->C + m0 * d->ldc * esz;
+    if (d->R) c.R = (const char*)d->R + m0 * d->ldr * 2;
+    if (d->MIX) c.MIX = (const char*)d->MIX + m0 * d->ldmix * 2;
+    if (d->rowbias) c.rowbias = d->rowbias + (m0 / d->rb_div) * d->ldrb;
+    c.orow_div = c.orow_stride = (int)mc;
+    const int rc = acth_gemm(&c, stream);
+    if (rc != ACTH_OK) return rc;
+  }
+  return ACTH_OK;
+}
+
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   if (!d || !d->A || !d->B || !d->C) return ACTH_EINVAL;
   // rows < 2^22: the epilogues divide row indices with a float-reciprocal estimate (udiv22)
@@ -229,7 +272,8 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   const long long a2_bytes = d->A2 ? ((a2_rows - 1) * (long long)d->lda2 +
                                       ((d->amode == 0 ? d->K : d->Cin) - c1)) * 2 : 0;
   const long long b_bytes = ((long long)(d->N - 1) * d->ldb + d->K) * 2;
-  if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL || b_bytes >= 0x80000000LL) return ACTH_EINVAL;
+  if (b_bytes >= 0x80000000LL) return ACTH_EINVAL;
+  if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL) return gemm_split_rows(d, stream);
   const int tile = choose_tile(d) & 0xff;
   if (tile == 4 || tile == 5)
     return gemm8p_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);

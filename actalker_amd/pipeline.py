@@ -139,13 +139,13 @@ class HipBackend:
         self.added = added_time_ids.to(dev, torch.float32)                                          # (nb, 3)
 
     def max_units_per_call(self) -> int:
-        """Largest UNet call (in 14-frame units) whose widest activation stays under the kernels'
-        2 GiB buffer extent (32-bit buffer offsets): level-0 rows x 4*C0 bf16 (the GEGLU hidden and
-        the Mamba xz rows; the Mamba sequence adds 33 condition tokens per frame, counted here
-        with margin as 64). 576x1024, C0 = 320: 90 frames -> 6 units."""
-        c0 = int(self.unet.config.block_out_channels[0])
-        per_unit = self.F * (self.S + 64) * 4 * c0 * 2
-        return max(1, (2 ** 31 - 1) // per_unit)
+        """Largest UNet call (in 14-frame units) the kernels take: GEMM rows < 2^22 (the epilogues'
+        float-reciprocal row division) at level 0, whose widest row count is the Mamba sequence (33
+        condition tokens per frame, counted with margin as 64). Operands past the 2 GiB buffer extent
+        (the 112-frame mode-2 call's 2.7 GB Mamba xz rows) are taken in row chunks by acth_gemm.
+        576x1024: 32 units (448 frames)."""
+        per_unit = self.F * (self.S + 64)
+        return max(1, ((1 << 22) - 1) // per_unit)
 
     def branch_twins(self) -> dict:
         """{branch: earlier branch with bitwise-identical UNet inputs}. The 4 CFG branches

@@ -312,6 +312,40 @@ def test_conv3x3(dev, B, H, W, C1, C2, Cout, mode):
     assert rel(out, refo.permute(0, 2, 3, 1).reshape(-1, Cout)) < 1e-2
 
 
+def test_gemm_over_2gib(dev):
+    """A operands past the 2 GiB buffer extent run as row chunks (acth_gemm's descriptor rebasing):
+    a strided dense A inside 4.5 GB rows (the mode-2 x_proj read of Mamba xz) with row-bias images and
+    residual, and a 3x3 conv over a 2.2 GB image batch; checked on rows / images at the chunk seams
+    against torch fp32 (rows are computed independently, so any row is as good as any other)."""
+    from actalker_amd.modules import pack_conv3x3
+    g = torch.Generator(device=dev).manual_seed(7)
+    M, K, LDA, N, RB = 1_100_000, 1024, 2048, 128, 9216
+    big = torch.randn(M, LDA, device=dev, generator=g, dtype=torch.float32).to(torch.bfloat16)
+    a = big[:, :K]                                   # 4.5 GB rows, 2.25 GB operand extent
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    rowb = torch.randn(-(-M // RB), N, device=dev, generator=g)
+    res = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    out = ops.gemm(a, w, rowbias=rowb, rb_div=RB, residual=res)
+    chunk = ((1 << 30) - 65536) // (RB * LDA) * RB   # first chunk's rows (whole row-bias images)
+    for r0 in (0, chunk - 700, chunk, M - 1000):
+        rows = slice(r0, r0 + 1000)
+        ref_rows = (a[rows].float() @ w.float().t() + rowb[torch.arange(r0, r0 + 1000, device=dev) // RB]
+                    + res[rows].float())
+        assert rel(out[rows], ref_rows) < 1e-2, r0
+    del big, a, res, out
+    torch.cuda.empty_cache()
+    # conv: 190 images of 72 x 128 x 640 -> 2.24 GB of A
+    B, H, W, Cin, Cout = 190, 72, 128, 640, 320
+    x = torch.randn(B * H * W, Cin, device=dev, generator=g).to(torch.bfloat16)
+    wc = (torch.randn(Cout, Cin, 3, 3, device=dev, generator=g) * (9 * Cin) ** -0.5).to(torch.bfloat16)
+    out = ops.conv3x3(x, pack_conv3x3(wc), B, H, W)
+    per = (1 << 30) // (H * W * Cin)                 # images per chunk
+    for b in (0, per - 1, per, B - 1):
+        img = x[b * H * W:(b + 1) * H * W].float().cpu().view(1, H, W, Cin).permute(0, 3, 1, 2)
+        refo = F.conv2d(img, wc.float().cpu(), padding=1).permute(0, 2, 3, 1).reshape(-1, Cout)
+        assert rel(out[b * H * W:(b + 1) * H * W], refo) < 1e-2, b
+
+
 def test_conv_temporal(dev):
     from actalker_amd.modules import pack_conv3d_t
     B, F_, H, W, C, Co = 2, 5, 6, 8, 128, 64

@@ -23,8 +23,6 @@
 // token (coalesced). xdbl rows (dt | B | C, fp32) are wave-uniform per token: staged in LDS per
 // tile of SC_T tokens, read back as broadcasts; the next tile is prefetched into registers while
 // the current one is scanned. State and exp(A) constants stay in registers.
-#include <stdlib.h>
-
 #include "common.h"
 
 #define SC_T 16
@@ -473,11 +471,6 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
   }
 }
 
-static bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] && v[0] != '0';
-}
-
 template <int R>
 static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
   const unsigned gx = (d.D + SC_THREADS - 1) / SC_THREADS;
@@ -486,20 +479,13 @@ static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
     // 32-channel one-wave blocks +2 % / +22 % / +22 % at levels 0 / 1 / 2; the 16 states split over
     // two waves with the xdbl row in SGPRs via scalar loads 1.9-3.2x slower, each token waiting
     // on its scalar loads.)
-    // Channel blocks of 320 for the level-0 width D = 640: every block stages the token tile's fp32
-    // xdbl row (dt | B | C) once, so wider blocks cut that re-read 2.5x (measured 3.98 -> 3.84 ms at
-    // nb 56, L 9249; at D = 1280 / 2560 the 128-channel blocks stay faster, 2.01 vs 2.12 ms and
-    // 1.38 vs 1.48 ms: profiles/r2_step6_bench_scan_ch{128,320}.log).
-    static const bool ch128 = getenv_flag("ACTH_SCAN_CH128");   // A/B switch (tools/bench_scan.py)
-    if (d.D == 640 && !ch128) {
-      const dim3 grid(d.D / 320, d.G, d.nb);
-      if (d.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 320, true>), grid, dim3(640), 0, stream, d);
-      else hipLaunchKernelGGL((scan_pair_kernel<R, 320, false>), grid, dim3(640), 0, stream, d);
-    } else {
-      const dim3 grid((d.D + 127) / 128, d.G, d.nb);
-      if (d.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true>), grid, dim3(256), 0, stream, d);
-      else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false>), grid, dim3(256), 0, stream, d);
-    }
+    // (320-channel blocks, which stage each token tile's fp32 xdbl row 2.5x less often, were measured
+    // and rejected: 3.84 vs 3.98 ms at nb 56, L 9249, but 7.31 vs 4.96 ms per level-0 call in the
+    // bench step (nb 84: 336 ten-wave blocks on 256 CUs run as two rounds; 840 four-wave blocks
+    // balance), profiles/r2_step6_bench_scan_ch*.log, r2_step7_kernel_stats.csv.)
+    const dim3 grid((d.D + 127) / 128, d.G, d.nb);
+    if (d.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true>), grid, dim3(256), 0, stream, d);
+    else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false>), grid, dim3(256), 0, stream, d);
   } else {
     // pass 1: every chunk but the last records its end state
     hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * (d.nchunks - 1)), dim3(SC_THREADS), 0, stream, d);

@@ -110,13 +110,14 @@ def gemm_algorithmic_bytes(a, w, M, N, K, kw):
     return a_elems * esz + N * K * esz + M * n_out * out_b + extra
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the GEMM launches measured by rocprofv3 PMC passes of this command
-    (tools/pmc_pass.sh -> tools/pmc_summary.py --json -> profiles/pmc_traffic.json), or None."""
+def pmc_traffic(family="acth_gemm"):
+    """Per-kernel-family HBM bytes measured by rocprofv3 PMC passes of this command over one sampler
+    step (tools/pmc_pass.sh -> tools/pmc_summary.py --json -> profiles/pmc_traffic.json), or None:
+    {hbm_bytes_per_launch (per kernel dispatch), dispatches, read_bytes, write_bytes, source}."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            return json.load(fh).get("acth_gemm")
+            return json.load(fh).get(family)
     except (OSError, ValueError):
         return None
 
@@ -257,7 +258,15 @@ class FamilyTimer:
             ach = work / (ms / 1e3) / scale
             out[fam] = dict(bound=bound, achieved=round(ach, 1), peak=pk, unit=unit, frac=round(ach / pk, 4),
                             launches=len(evs), avg_launch_us=round(1000.0 * ms / len(evs), 1),
-                            share_of_step=round(ms / step_ms_total, 4))
+                            share_of_step=round(ms / step_ms_total, 4),
+                            algorithmic_bytes_or_flop_per_launch=round(work / len(evs)))
+            pmc = pmc_traffic(fam)
+            if pmc:
+                # PMC bytes per kernel dispatch x dispatches per op call (GroupNorm: stats + apply)
+                per_call = 2 if fam == "groupnorm" else 1
+                out[fam]["traffic"] = round(pmc["hbm_bytes_per_launch"] * per_call)
+                out[fam]["traffic_unit"] = "HBM bytes per op call (PMC 2*FETCH_SIZE + WRITE_SIZE)"
+                out[fam]["traffic_source"] = pmc.get("source")
         return out
 
 

@@ -10,8 +10,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from actalker_amd import ops  # noqa: E402
 
-# (nb, L, D = 2C, R): audio branch at levels 0 / 1 / 2 (S + 33 tokens)
-SHAPES = [(56, 9249, 640, 20), (56, 2337, 1280, 40), (56, 609, 2560, 80)]
+# (nb, L, D = 2C, R): audio branch at levels 0 / 1 / 2 (S + 33 tokens); nb as in the bench step
+# (grid quantisation over 256 CUs depends on nb: measure at the real nb)
+SHAPES = [(84, 9249, 640, 20), (84, 2337, 1280, 40), (84, 609, 2560, 80)]   # the bench step: 6 units x 14 frames
 
 
 def main(iters=3):

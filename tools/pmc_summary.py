@@ -36,12 +36,19 @@ def main():
         import json
         out = sys.argv[sys.argv.index("--json") + 1]
         src = sys.argv[sys.argv.index("--source") + 1] if "--source" in sys.argv else d
-        g = [r for r in rows if "gemm" in r[0]]
-        n = sum(r[1] for r in g)
+        fams = {"acth_gemm": lambda k: "gemm" in k, "flash_attn": lambda k: "flash_attn" in k,
+                "selective_scan": lambda k: "scan" in k, "groupnorm": lambda k: k.startswith("gn_"),
+                "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k}
+        res = {}
+        for fam, match in fams.items():
+            g = [r for r in rows if match(r[0].split("(")[0].replace("void ", ""))]
+            n = sum(r[1] for r in g)
+            if not n:
+                continue
+            res[fam] = {"hbm_bytes_per_launch": sum(r[2] + r[3] for r in g) / n, "dispatches": n,
+                        "read_bytes": sum(r[2] for r in g), "write_bytes": sum(r[3] for r in g), "source": src}
         with open(out, "w") as fh:
-            json.dump({"acth_gemm": {"hbm_bytes_per_launch": sum(r[2] + r[3] for r in g) / max(n, 1),
-                                     "dispatches": n, "read_bytes": sum(r[2] for r in g),
-                                     "write_bytes": sum(r[3] for r in g), "source": src}}, fh, indent=1)
+            json.dump(res, fh, indent=1)
         return
     w = csv.writer(sys.stdout)
     w.writerow(["Name", "Dispatches", "ReadBytesTotal", "WriteBytesTotal", "HbmBytesPerDispatch"])

@@ -335,11 +335,43 @@ class IPAdapterAttnProcessor2_0(Packed):
 
     def w_kv(self, i):
         """to_k_ip[i] | to_v_ip[i] fused as one (2C, cross_dim) weight."""
-        return self._pk(("kv", i), lambda: _bf(torch.cat([self.to_k_ip[i].weight, self.to_v_ip[i].weight], 0)))
+        return ip_w_kv(self, i)
 
 
 def _scale_value(s) -> float:
     return float(s[0]) if isinstance(s, (list, tuple)) else float(s)
+
+
+def is_ip_processor(proc) -> bool:
+    """An IP-adapter processor: ours, or the reference's own IPAdapterAttnProcessor2_0 object that the
+    reference's unmodified ``add_ip_adapters`` (unet_spatio_temporal_condition.py:519-566) installs
+    through ``set_attn_processor`` -- anything with ``to_k_ip`` / ``to_v_ip`` lists and ``scale``."""
+    return hasattr(proc, "to_k_ip") and hasattr(proc, "to_v_ip") and hasattr(proc, "scale")
+
+
+def _versioned_pack(mod: nn.Module, key, tensors, fn):
+    """Kernel-layout pack cached on ``mod`` and keyed on the source tensors' in-place version counters,
+    so a later ``load_state_dict`` into a foreign processor (the reference's ``load_adapter_states``)
+    invalidates it without any hook of ours."""
+    cache = mod.__dict__.setdefault("_acth_vcache", {})
+    ver = tuple((t.data_ptr(), t._version) for t in tensors)
+    hit = cache.get(key)
+    if hit is None or hit[0] != ver:
+        with torch.no_grad():
+            hit = (ver, fn())
+        cache[key] = hit
+    return hit[1]
+
+
+def ip_w_kv(proc, i):
+    """to_k_ip[i] | to_v_ip[i] fused as one (2C, cross_dim) bf16 weight."""
+    k, v = proc.to_k_ip[i].weight, proc.to_v_ip[i].weight
+    return _versioned_pack(proc, ("kv", i), (k, v), lambda: _bf(torch.cat([k, v], 0)))
+
+
+def ip_w_v(proc, i):
+    v = proc.to_v_ip[i].weight
+    return _versioned_pack(proc, ("v", i), (v,), lambda: _bf(v))
 
 
 class Attention(Packed):
@@ -391,14 +423,14 @@ class Attention(Packed):
         # softmax over a single key is exactly 1: the ID attention is to_v(ID) broadcast
         v_id = ops.gemm(id_tok, self.to_v.w())
         proc = self.processor
-        if isinstance(proc, IPAdapterAttnProcessor2_0):
+        if is_ip_processor(proc):
             sa, sb = _scale_value(proc.scale[0]), _scale_value(proc.scale[1])
             q = kv = vb = None
             if use_a and sa != 0.0:
                 q = ops.gemm(n, self.to_q.w())
-                kv = ops.gemm(audio, proc.w_kv(0))
+                kv = ops.gemm(audio, ip_w_kv(proc, 0))
             if use_b and sb != 0.0:
-                vb = ops.gemm(vasa, proc.to_v_ip[1].w())
+                vb = ops.gemm(vasa, ip_w_v(proc, 1))
             comb = ops.ip_attn(v_id, M, self.heads, rows_per_ctx, S, q=q, kv=kv, nkeys=ctx.n_audio, vb=vb,
                                mask_a=ma, mask_b=mb, sa=sa, sb=sb)
         else:

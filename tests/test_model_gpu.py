@@ -79,6 +79,70 @@ def test_unet_forward_matches_oracle(dev, tiny, masks_kind):
     assert err < 5e-2, err
 
 
+class _RefAttnProcessor2_0(torch.nn.Module):
+    """Stand-in with the reference's attribute surface (attention_processor.py:1518-1527): no params."""
+
+
+class _RefIPAdapterAttnProcessor2_0(torch.nn.Module):
+    """Stand-in with the reference IPAdapterAttnProcessor2_0's attribute surface (attention_processor.py:
+    2717-2745): plain torch Linear lists ``to_k_ip`` / ``to_v_ip``, ``scale`` and ``num_tokens`` lists."""
+
+    def __init__(self, hidden_size, cross_attention_dim, num_tokens, scale):
+        super().__init__()
+        self.hidden_size, self.cross_attention_dim = hidden_size, cross_attention_dim
+        self.num_tokens, self.scale = num_tokens, scale
+        self.to_k_ip = torch.nn.ModuleList([torch.nn.Linear(cross_attention_dim, hidden_size, bias=False)
+                                            for _ in num_tokens])
+        self.to_v_ip = torch.nn.ModuleList([torch.nn.Linear(cross_attention_dim, hidden_size, bias=False)
+                                            for _ in num_tokens])
+
+
+def test_reference_processor_objects_drive_the_unet(dev):
+    """The reference's unmodified add_ip_adapters / load_adapter_states (unet_spatio_temporal_condition.py:
+    519-591) hand the UNet the reference's own processor objects through set_attn_processor and then load
+    weights into them: the HIP UNet runs them as its own (same output bitwise, same state_dict keys) and
+    picks up weights loaded into them afterwards (packs keyed on the tensors' version counters)."""
+    unet, cfg = ge._tiny_unet(seed=11)
+    unet = unet.to(dev)
+    sample, t, ehs, added, pose, masks = ge._tiny_inputs(B=1, F=3, H=16, W=32, seed=6)
+    args = (sample.to(dev), t.to(dev), (ehs[0].to(dev), [e.to(dev) for e in ehs[1]]), added.to(dev))
+    kw = dict(spatial_condition=pose.to(dev), cross_attention_kwargs={"ip_adapter_masks": masks}, return_dict=False)
+    ours = unet(*args, **kw)[0]
+    keys = sorted(unet.state_dict().keys())
+    procs = {}
+    for name, p in unet.attn_processors.items():
+        if hasattr(p, "to_k_ip"):
+            q = _RefIPAdapterAttnProcessor2_0(p.hidden_size, p.cross_attention_dim, [32, 32], [1.25, 1.25]).to(dev)
+            q.load_state_dict({k: v.detach().clone() for k, v in p.state_dict().items()})
+            procs[name] = q
+        else:
+            procs[name] = _RefAttnProcessor2_0()
+    unet.set_attn_processor(procs)
+    assert sorted(unet.state_dict().keys()) == keys
+    got = unet(*args, **kw)[0]
+    assert torch.equal(got, ours)
+    # load_adapter_states-style in-place load into the foreign modules
+    adapters = torch.nn.ModuleList([m for m in unet.attn_processors.values()
+                                    if isinstance(m, _RefIPAdapterAttnProcessor2_0)])
+    sd = {k: (0.5 * v) if ".to_v_ip.0." in k else v for k, v in adapters.state_dict().items()}
+    adapters.load_state_dict(sd)
+    changed = unet(*args, **kw)[0]
+    assert not torch.equal(changed, ours)
+    # the same weights through the build's own processors give the same output
+    own = {}
+    for name, p in unet.attn_processors.items():
+        if hasattr(p, "to_k_ip"):
+            from actalker_amd.modules import IPAdapterAttnProcessor2_0
+            q = IPAdapterAttnProcessor2_0(p.hidden_size, p.cross_attention_dim, [32, 32], [1.25, 1.25]).to(dev)
+            q.load_state_dict({k: v.detach().clone() for k, v in p.state_dict().items()})
+            own[name] = q
+        else:
+            from actalker_amd.modules import AttnProcessor2_0
+            own[name] = AttnProcessor2_0()
+    unet.set_attn_processor(own)
+    assert torch.equal(unet(*args, **kw)[0], changed)
+
+
 def test_unet_gate_hint_is_exact(dev, tiny):
     """The pipeline's gate hint only skips work whose result is exactly zero."""
     unet, sd, cfg = tiny

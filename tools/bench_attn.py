@@ -10,7 +10,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from actalker_amd import ops  # noqa: E402
 
-SHAPES = [(56, 9216, 5), (56, 2304, 10), (56, 576, 20), (56, 144, 20)]   # (frames, tokens, heads)
+SHAPES = [(84, 9216, 5), (84, 2304, 10), (84, 576, 20), (84, 144, 20)]   # (frames, tokens, heads): the bench step
 
 
 def main(iters=5):

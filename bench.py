@@ -37,7 +37,8 @@ sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
 PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s achievable)
-TFLOP_PER_FRAME_FWD = 3.433        # SURVEY.md 8(d), 576x1024, mode 2 (modes 0/1: 3.402)
+# algorithmic TFLOP per UNet frame-forward: (height, width, mode 2?)
+TFLOP_PER_FRAME_FWD = {(576, 1024, True): 3.433, (576, 1024, False): 3.402, (576, 576, False): 1.779}
 MODES = {0: ([1, 0], "mode=0 audio-only"), 1: ([0, 1], "mode=1 expression-only"), 2: ([1, 1], "mode=2 audio+expression")}
 
 
@@ -448,7 +449,8 @@ def main():
                        "model": "SVD-XT UNet + ACTalker v10 dual-Mamba (1.775B, random init)",
                        "global_batch": N, "seq_len": fpb, "parallelism": f"units{world}"},
             "unet_frame_forwards_per_s_per_gpu": round(frame_fwds / elapsed, 3),
-            "achieved_mfma_tflops_whole_step": round(frame_fwds * TFLOP_PER_FRAME_FWD / elapsed, 1),
+            "achieved_mfma_tflops_whole_step": (round(frame_fwds * TFLOP_PER_FRAME_FWD[(H, W, args.mode == 2)] / elapsed, 1)
+                                                if (H, W, args.mode == 2) in TFLOP_PER_FRAME_FWD else None),
             "cfg_branches_evaluated": len(branches),
             "all_four_branches": four,
             "finite": ok,

@@ -50,6 +50,22 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // the GEGLU epilogue of the K = 320 / 640 GEMMs is VALU-bound on this math.
 typedef float float2_pk __attribute__((ext_vector_type(2)));
 
+// The same GELU from the degree-8 erf fit of ffn.hip (erf(g / sqrt 2) = gc * Q(gc^2), gc = g clamped to
+// +-2.95 sqrt 2, |GELU error| <= 7.4e-5): 12 packed ops per pair instead of 16.
+__device__ __forceinline__ float2_pk gelu_pk8(float2_pk x) {
+  constexpr float c[9] = {0.7977727652f, -0.1326450109f, 0.01961599849f, -0.002216302557f, 1.874310692e-04f,
+                          -1.138649350e-05f, 4.631291688e-07f, -1.116308557e-08f, 1.195545885e-10f};
+  float2_pk gc;
+  gc.x = __builtin_amdgcn_fmed3f(x.x, -4.171930f, 4.171930f);
+  gc.y = __builtin_amdgcn_fmed3f(x.y, -4.171930f, 4.171930f);
+  const float2_pk v = gc * gc;
+  float2_pk r = {c[8], c[8]};
+#pragma unroll
+  for (int k = 7; k >= 0; --k) r = __builtin_elementwise_fma(r, v, (float2_pk){c[k], c[k]});
+  const float2_pk hx = x * (float2_pk){0.5f, 0.5f};
+  return __builtin_elementwise_fma(hx, gc * r, hx);
+}
+
 __device__ __forceinline__ float2_pk gelu_pk(float2_pk x) {
   constexpr float c[12] = {1.128378868e+00f, -3.761171401e-01f, 1.127940044e-01f, -2.678386122e-02f,
                            5.143333692e-03f, -8.073762292e-04f, 1.023587902e-04f, -1.013244946e-05f,
@@ -64,6 +80,10 @@ __device__ __forceinline__ float2_pk gelu_pk(float2_pk x) {
   const float2_pk hx = x * (float2_pk){0.5f, 0.5f};
   return __builtin_elementwise_fma(hx, z * r, hx);
 }
+
+#ifndef GEGLU_GELU
+#define GEGLU_GELU gelu_pk8
+#endif
 
 __device__ __forceinline__ float softplus_f(float x) {
   // torch.nn.functional.softplus(beta=1, threshold=20)

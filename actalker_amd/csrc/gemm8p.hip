@@ -394,7 +394,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
           }
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
-            const float2_pk gg = gelu_pk((float2_pk){gt[e], gt[e + 1]});
+            const float2_pk gg = GEGLU_GELU((float2_pk){gt[e], gt[e + 1]});
             v[e] = h[e] * gg.x;
             v[e + 1] = h[e + 1] * gg.y;
           }

@@ -260,7 +260,7 @@ __device__ __forceinline__ void epilogue_geglu8(const ActhGemmDesc& p, int row, 
   }
 #pragma unroll
   for (int e = 0; e < 8; e += 2) {
-    const float2_pk gg = gelu_pk((float2_pk){gv[e], gv[e + 1]});
+    const float2_pk gg = GEGLU_GELU((float2_pk){gv[e], gv[e + 1]});
     v[e] = hv[e] * gg.x;
     v[e + 1] = hv[e + 1] * gg.y;
   }

@@ -230,6 +230,10 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
     static_for<0, NS>([&](auto s_c) {
       constexpr int s = decltype(s_c)::value;
       load(std::integral_constant<int, s + 3>{});
+      // the up projection's MFMA run at raised priority (the partner wave's gate VALU fills its shadow):
+      // -1 % per chunk (profiles/r2_step9_ffn_stamps_prio.log)
+      if constexpr (s == 0) __builtin_amdgcn_s_setprio(1);
+      if constexpr (s == KS) __builtin_amdgcn_s_setprio(0);
       if constexpr (DN && s == KS - 6) hpar = *reinterpret_cast<const bf16x8_t*>(hxr);
       if constexpr (s < KS) {
         if constexpr (UP) u = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s & 3], xf[s], u, 0, 0, 0);

@@ -483,9 +483,15 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim, activation_fn="geglu")
 
     def run(self, ctx: Ctx, h, S):
+        return self.run_after_attn1(ctx, self.run_attn1(ctx, h, S), S)
+
+    def run_attn1(self, ctx: Ctx, h, S):
+        """attn1(norm1(h)) + h: the part that reads no IP-adapter (audio / VASA / ID) input."""
         n = ops.layernorm(h, *self.norm1.gb(), self.norm1.eps)
-        h = self.attn1.run_self(ctx, n, h, S, temporal=False)
-        n = ops.layernorm(h, *self.norm2.gb(), self.norm2.eps, out=n)
+        return self.attn1.run_self(ctx, n, h, S, temporal=False)
+
+    def run_after_attn1(self, ctx: Ctx, h, S):
+        n = ops.layernorm(h, *self.norm2.gb(), self.norm2.eps)
         h = self.attn2.run_cross(ctx, n, h, S, temporal=False)
         n = ops.layernorm(h, *self.norm3.gb(), self.norm3.eps, out=n)
         return self.ff.run(n, h)
@@ -680,16 +686,24 @@ class TransformerSpatioTemporalModel(nn.Module):
         fidx = torch.arange(ctx.F, device=ctx.device, dtype=torch.float32).repeat(ctx.B)
         return self.time_pos_embed.run(self.time_proj.run(fidx))
 
-    def run(self, ctx: Ctx, x, H, W):
+    def run(self, ctx: Ctx, x, H, W, prefix=None):
+        """``prefix`` = (ctx_u, expand): ``x`` holds only the batch elements of ``ctx_u`` (the distinct
+        CFG-prefix inputs, see UNet.forward_tokens); everything before the first IP-adapter input (GroupNorm,
+        proj_in, the first block's attn1) runs on them, then ``expand`` copies the rows out to ``ctx``'s
+        full batch."""
         S = H * W
         g, b = self.norm.gb()
+        cin = ctx if prefix is None else prefix[0]
         n = ops.groupnorm(x, g, b, self.norm.eps, S)
         h = ops.gemm(n, self.proj_in.w(), bias=self.proj_in.b())
         del n
+        if prefix is not None:
+            h = prefix[1](self.transformer_blocks[0].run_attn1(cin, h, S))
+            x = prefix[1](x)
         pos = self._pos_emb(ctx)
         alpha = self.time_mixer.alpha()
         for i, (blk, tblk) in enumerate(zip(self.transformer_blocks, self.temporal_transformer_blocks)):
-            h = blk.run(ctx, h, S)
+            h = blk.run_after_attn1(ctx, h, S) if (prefix is not None and i == 0) else blk.run(ctx, h, S)
             if self.has_mamba:
                 h = self.mamba_blocks[i].run(ctx, h, S)
             h = tblk.run(ctx, h, pos, S, alpha)
@@ -776,11 +790,17 @@ class CrossAttnDownBlockSpatioTemporal(nn.Module):
         self.downsamplers = (nn.ModuleList([Downsample2D(out_channels, use_conv=True, out_channels=out_channels,
                                                          padding=1, name="op")]) if add_downsample else None)
 
-    def run(self, ctx, h, H, W):
+    def run(self, ctx, h, H, W, prefix=None):
+        """``prefix``: see TransformerSpatioTemporalModel.run -- ``h`` then holds the distinct-prefix batch
+        and the first resnet runs on it too."""
         outs = []
-        for res, attn in zip(self.resnets, self.attentions):
-            h = res.run(ctx, h, H, W)
-            h = attn.run(ctx, h, H, W)
+        for i, (res, attn) in enumerate(zip(self.resnets, self.attentions)):
+            if prefix is not None and i == 0:
+                h = res.run(prefix[0], h, H, W)
+                h = attn.run(ctx, h, H, W, prefix=prefix)
+            else:
+                h = res.run(ctx, h, H, W)
+                h = attn.run(ctx, h, H, W)
             outs.append(h)
         if self.downsamplers is not None:
             h = self.downsamplers[0].run(ctx, h, H, W)

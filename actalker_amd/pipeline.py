@@ -124,6 +124,8 @@ class HipBackend:
         self.T, self.F = T, fpb
         self.masks = gate_masks(gate, *masks)
         self.gate = list(gate)
+        # run the UNet prefix once per (window, prefix class) inside a call (LoopConfig.share_cfg_prefix)
+        self.share_prefix = True
         nb = image_latents.shape[0]
         # conditioning in device layouts, converted once per run
         self.img = ops.nchw_to_tokens(image_latents.to(dev).float(), out_dtype=torch.float32)     # (nb*T*S, 4)
@@ -146,6 +148,23 @@ class HipBackend:
         576x1024: 32 units (448 frames)."""
         per_unit = self.F * (self.S + 64)
         return max(1, ((1 << 22) - 1) // per_unit)
+
+    def prefix_classes(self) -> List[int]:
+        """Per CFG branch, the first branch whose UNet prefix inputs are bitwise equal (image latents and
+        added time ids; the window's noisy latents, timestep and pose rows are shared by construction).
+        Branches 1-3 (drop audio+vasa, drop vasa, cond) share them (pipeline:162-200, 186-205), so the
+        UNet prefix before the first IP-adapter input runs once per window for them."""
+        if getattr(self, "_prefix_cls", None) is None:
+            nb = self.ide.shape[0]
+            img = self.img.reshape(nb, -1)
+            cls = list(range(nb))
+            for c in range(1, nb):
+                for e in range(c):
+                    if cls[e] == e and torch.equal(img[c], img[e]) and torch.equal(self.added[c], self.added[e]):
+                        cls[c] = e
+                        break
+            self._prefix_cls = cls
+        return self._prefix_cls
 
     def branch_twins(self) -> dict:
         """{branch: earlier branch with bitwise-identical UNet inputs}. The 4 CFG branches
@@ -196,9 +215,14 @@ class HipBackend:
         if self.pose_P != self.T:
             pr = torch.tensor([r % self.pose_P for (w, _c) in units for r in self._raw[w]], dtype=torch.int32)
             prmap, pmax = pr.to(self.dev, non_blocking=True), int(pr.max())
+        prefix_src = None
+        if self.share_prefix:
+            cls = self.prefix_classes()
+            first = {}
+            prefix_src = [first.setdefault((w, cls[c]), b) for b, (w, c) in enumerate(units)]
         noise = self.unet.forward_tokens(x, U, F, self.H, self.W, tt, ehs, self.added[br_d], self.pose, cak,
                                          spatial_condition_rmap=prmap, out_f32=True,
-                                         spatial_condition_rmap_max=pmax)
+                                         spatial_condition_rmap_max=pmax, prefix_src=prefix_src)
         out[row0:row0 + U * F * S].copy_(noise)
 
     def step_windows(self, lat, gathered, unit_rows: List[List[int]], frames, guidance, sigma, sigma_next):
@@ -258,6 +282,9 @@ class LoopConfig:
     concurrent_calls: int = 1
     # evaluate a CFG branch whose inputs are bitwise those of another branch once (backend.branch_twins)
     dedup_branches: bool = True
+    # run the UNet prefix before the first IP-adapter input once per window for the CFG branches that
+    # share its inputs (backend.prefix_classes; branches 1-3), inside each UNet call
+    share_cfg_prefix: bool = True
 
 
 def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, world: int = 1,
@@ -277,6 +304,8 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
         broadcast_from_rank0(lat, group)
     n_windows = len(range(0, T, F - cfg.overlap))
     twins = backend.branch_twins() if (cfg.dedup_branches and hasattr(backend, "branch_twins")) else {}
+    if hasattr(backend, "share_prefix"):
+        backend.share_prefix = cfg.share_cfg_prefix
     branches = [c for c in range(4) if c not in twins]
     my_units, cap = assign_units(n_windows, world, rank, branches=branches)
     owners = unit_owner(n_windows, world, branches=branches)

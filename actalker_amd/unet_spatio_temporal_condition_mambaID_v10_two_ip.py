@@ -16,7 +16,7 @@ from __future__ import annotations
 import json
 import os
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional, Tuple, Union
+from typing import Sequence, Any, Dict, List, Optional, Tuple, Union
 
 import torch
 import torch.nn as nn
@@ -309,31 +309,85 @@ class UNetSpatioTemporalConditionModel(nn.Module):
                        added_time_ids, spatial_condition_tok: Optional[torch.Tensor] = None,
                        cross_attention_kwargs: Optional[Dict[str, Any]] = None,
                        spatial_condition_rmap: Optional[torch.Tensor] = None, out_f32: bool = True,
-                       spatial_condition_rmap_max: Optional[int] = None):
+                       spatial_condition_rmap_max: Optional[int] = None,
+                       prefix_src: Optional[Sequence[int]] = None):
         """Token-major entry: x_tok (B*F*H*W, in_channels) bf16 -> (B*F*H*W, out_channels).
         ``spatial_condition_rmap`` (device int32, one entry per frame) remaps frame rows of
-        ``spatial_condition_tok``; ``spatial_condition_rmap_max`` is the host-side bound on its entries."""
+        ``spatial_condition_tok``; ``spatial_condition_rmap_max`` is the host-side bound on its entries.
+
+        ``prefix_src`` (host list, one entry per batch element): batch element b computes the UNet prefix
+        that reads no IP-adapter input -- conv_in, the first down block's first ResBlock, the first
+        transformer's GroupNorm / proj_in and its first block's attn1 -- as element prefix_src[b] <= b
+        does. The caller guarantees those elements' latent rows, spatial condition rows, timestep and
+        added time ids are equal (the pipeline's CFG branches 1-3 of one window differ only in the audio /
+        VASA / ID prompts, pipeline:162-200); the prefix then runs once per distinct element and its
+        rows are copied out (exact: every op there is per batch element)."""
         if self.device.type != "cuda":
             raise RuntimeError("UNetSpatioTemporalConditionModel (actalker_amd) runs on the MI355X HIP kernels "
                                "only; move it to a GPU device first")
         ctx = self._prep_ctx(B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs)
-        BF = B * F
         S0 = H * W
+        uniq = None
+        if prefix_src is not None and len(prefix_src) == B and self._prefix_capable():
+            if any(prefix_src[b] > b or prefix_src[prefix_src[b]] != prefix_src[b] for b in range(B)):
+                raise ValueError("prefix_src[b] must be <= b and name a distinct element")
+            uniq = [b for b in range(B) if prefix_src[b] == b]
+            if len(uniq) == B:
+                uniq = None
+        prefix = None
+        if uniq is not None:
+            Bu = len(uniq)
+            pos = {b: i for i, b in enumerate(uniq)}
+            ui = torch.tensor(uniq, dtype=torch.int64, device=x_tok.device)
+            inv = torch.tensor([pos[prefix_src[b]] for b in range(B)], dtype=torch.int64, device=x_tok.device)
+
+            def take(t, per):                # rows of the distinct elements (t holds B x per rows)
+                return t.reshape(B, per, *t.shape[1:]).index_select(0, ui).reshape(Bu * per, *t.shape[1:])
+
+            def expand(t):                   # distinct-element rows -> the full batch
+                per = t.shape[0] // Bu
+                return t.reshape(Bu, per, *t.shape[1:]).index_select(0, inv).reshape(B * per, *t.shape[1:])
+
+            if isinstance(encoder_hidden_states, tuple):
+                ehs_u = (take(encoder_hidden_states[0], F), [take(e, F) for e in encoder_hidden_states[1]])
+            else:
+                ehs_u = take(encoder_hidden_states, F)
+            added_u = added_time_ids.reshape(B, -1).index_select(0, ui.to(added_time_ids.device))
+            t_u = timestep
+            if torch.is_tensor(timestep) and timestep.numel() == B:
+                t_u = timestep.reshape(-1).index_select(0, ui.to(timestep.device))
+            ctx_u = self._prep_ctx(Bu, F, t_u, ehs_u, added_u, cross_attention_kwargs)
+            prefix = (ctx_u, expand)
+            x_in = take(x_tok, F * S0)
+            rmap_in = take(spatial_condition_rmap, F) if spatial_condition_rmap is not None else None
+            sc_in = spatial_condition_tok
+            if sc_in is not None and rmap_in is None and sc_in.shape[0] == B * F * S0:
+                sc_in = take(sc_in, F * S0)            # per-element rows (no frame remap)
+            B_in = Bu
+        else:
+            x_in, rmap_in, sc_in, B_in = x_tok, spatial_condition_rmap, spatial_condition_tok, B
         # conv_in (+ spatial_condition add fused as the residual)
-        cols = ops.im2col3x3(x_tok, BF, H, W)
+        cols = ops.im2col3x3(x_in, B_in * F, H, W)
         kw = {}
-        if spatial_condition_tok is not None:
-            kw = dict(residual=spatial_condition_tok)
-            if spatial_condition_rmap is not None:
+        if sc_in is not None:
+            kw = dict(residual=sc_in)
+            if rmap_in is not None:
                 # row (u*F + f)*S0 + s reads spatial_condition row rmap[u*F + f]*S0 + s
                 if spatial_condition_rmap_max is None:
                     raise ValueError("spatial_condition_rmap needs spatial_condition_rmap_max")
-                kw.update(rmap=spatial_condition_rmap, r_div=S0, r_mod=spatial_condition_rmap.numel(),
-                          rmap_max=spatial_condition_rmap_max)
+                kw.update(rmap=rmap_in, r_div=S0, r_mod=rmap_in.numel(), rmap_max=spatial_condition_rmap_max)
         h = ops.gemm(cols, self._conv_in_w(), bias=self.conv_in.b(), **kw)
         del cols
-        skips = [h]
-        for blk in self.down_blocks:
+        BF = B * F
+        if prefix is not None:
+            skips = [expand(h)]
+            h, outs, H, W = self.down_blocks[0].run(ctx, h, H, W, prefix=prefix)
+            skips.extend(outs)
+            rest = self.down_blocks[1:]
+        else:
+            skips = [h]
+            rest = self.down_blocks
+        for blk in rest:
             h, outs, H, W = blk.run(ctx, h, H, W)
             skips.extend(outs)
         h = self.mid_block.run(ctx, h, H, W)
@@ -342,6 +396,11 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         g, b = self.conv_norm_out.gb()
         n = ops.groupnorm(h, g, b, self.conv_norm_out.eps, H * W, silu=True)
         return ops.conv3x3(n, self.conv_out.w3(), BF, H, W, bias=self.conv_out.b(), out_f32=out_f32)
+
+    def _prefix_capable(self) -> bool:
+        from .modules import CrossAttnDownBlockSpatioTemporal
+        b0 = self.down_blocks[0]
+        return isinstance(b0, CrossAttnDownBlockSpatioTemporal) and len(b0.attentions) > 0
 
     def _conv_in_w(self):
         # conv_in has Cin = 8 < 64: explicit im2col + dense GEMM, weight as (Cout, 9*Cin)

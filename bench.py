@@ -323,6 +323,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-share-prefix", action="store_true",
+                    help="run the UNet prefix before the first IP-adapter input for every CFG branch (no sharing "
+                         "between the branches whose prefix inputs are equal)")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
     ap.add_argument("--no-four-branch-compare", action="store_true",
@@ -362,7 +365,7 @@ def main():
                             inp["vasa_prompts"], inp["pose_fea"])
     cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7,
                         concurrent_calls=args.concurrent_calls, dedup_branches=not args.no_dedup,
-                        units_per_call=args.units_per_call)
+                        units_per_call=args.units_per_call, share_cfg_prefix=not args.no_share_prefix)
     twins = backend.branch_twins() if cfg.dedup_branches else {}
     branches = [c for c in range(4) if c not in twins]
     log(f"CFG branches evaluated: {branches} (twins {twins})")
@@ -421,7 +424,7 @@ def main():
     if twins and world == 1 and not args.no_four_branch_compare:
         cfg4 = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7,
                              concurrent_calls=args.concurrent_calls, dedup_branches=False,
-                             units_per_call=args.units_per_call)
+                             units_per_call=args.units_per_call, share_cfg_prefix=False)
         with torch.no_grad():
             pl.denoise(backend, inp["latents"], cfg4, rank, world, group, steps=1)
         barrier()
@@ -452,6 +455,7 @@ def main():
             "achieved_mfma_tflops_whole_step": (round(frame_fwds * TFLOP_PER_FRAME_FWD[(H, W, args.mode == 2)] / elapsed, 1)
                                                 if (H, W, args.mode == 2) in TFLOP_PER_FRAME_FWD else None),
             "cfg_branches_evaluated": len(branches),
+            "cfg_prefix_shared": cfg.share_cfg_prefix,
             "all_four_branches": four,
             "finite": ok,
             "roofline": roof,

@@ -143,6 +143,62 @@ def test_reference_processor_objects_drive_the_unet(dev):
     assert torch.equal(unet(*args, **kw)[0], changed)
 
 
+def test_cfg_prefix_sharing_matches_full_batch(dev, tiny):
+    """forward_tokens(prefix_src=...): batch elements whose prefix inputs are equal (latent + image rows,
+    pose, timestep, added time ids) run conv_in .. the first attn1 once; outputs match the unshared call
+    (rows are computed per element; only GEMM tile choices for the smaller M may differ)."""
+    from actalker_amd import ops
+    unet, sd, cfg = tiny
+    sample, t, ehs, added, pose, masks = ge._tiny_inputs(B=3, F=3, H=16, W=32, seed=8)
+    sample[2] = sample[1]                              # elements 1, 2: same prefix inputs,
+    added[2] = added[1]                                # different audio / VASA / ID prompts
+    pose[2] = pose[1]
+    B, F, H, W = 3, 3, 16, 32
+    x = ops.nchw_to_tokens(sample.to(dev))
+    sc = ops.nchw_to_tokens(pose.to(dev))
+    e = (ehs[0].to(dev), [a.to(dev) for a in ehs[1]])
+    cak = {"ip_adapter_masks": masks}
+    with torch.no_grad():
+        full = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak)
+        shared = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak, prefix_src=[0, 1, 1])
+        shared_none = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak, prefix_src=[0, 1, 2])
+    assert torch.equal(shared_none, full)
+    assert rel(shared, full) < 1e-3
+    with pytest.raises(ValueError):
+        unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak, prefix_src=[0, 2, 2])
+
+
+def test_pipeline_prefix_sharing_matches_unshared_loop(dev, tiny):
+    """The sampler loop with LoopConfig.share_cfg_prefix on and off, CFG inputs shaped as the reference
+    builds them (pipeline:162-205: branch 0 zero image latents / ID, branches 1-3 equal image latents;
+    mode 2, so all four branches run and 1-3 share the prefix)."""
+    from actalker_amd import pipeline as pl
+    unet, sd, cfg = tiny
+    N, fpb, H, W = 4, 2, 16, 32
+    T = N + fpb
+    g = torch.Generator().manual_seed(23)
+    latents = 0.18215 * torch.randn(1, 1, 4, H, W, generator=g) + 700.0 * torch.randn(1, T, 4, H, W, generator=g)
+    img1 = torch.randn(1, T, 4, H, W, generator=g)
+    imgl = torch.cat([torch.zeros_like(img1), img1, img1, img1])
+    ide1 = torch.randn(1, T, 1, 1024, generator=g)
+    ide = torch.cat([torch.zeros_like(ide1), ide1, ide1, ide1])
+    aud = torch.randn(4, T, 32, 1024, generator=g)
+    vas = torch.randn(4, T, 1, 1024, generator=g)
+    pose = 0.1 * torch.randn(1, T, 64, H, W, generator=g)
+    added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
+    lower = torch.zeros(1, 1, 8 * H, 8 * W)
+    lower[..., 4 * H:, :] = 1.0
+    masks = (torch.ones(1, 1, 8 * H, 8 * W), lower, 1 - lower)
+    outs = []
+    for share in (True, False):
+        backend = pl.HipBackend(unet, H, W, masks, [1, 1], added, T, fpb, imgl, ide, aud, vas, pose)
+        assert backend.prefix_classes() == [0, 1, 1, 1]
+        lc = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, share_cfg_prefix=share)
+        with torch.no_grad():
+            outs.append(pl.denoise(backend, latents, lc, steps=2))
+    assert rel(outs[0], outs[1]) < 2e-3
+
+
 def test_unet_gate_hint_is_exact(dev, tiny):
     """The pipeline's gate hint only skips work whose result is exactly zero."""
     unet, sd, cfg = tiny

@@ -308,6 +308,7 @@ __device__ __forceinline__ void gn_finish(const ActhGroupNormDesc& p, long long 
   *reinterpret_cast<uint4*>((bf16_t*)p.y + row * p.ldy + ch * 8) = pack8(v);
 }
 
+#define GN_MAX_GROUPS 1024
 // grid: M / rows_per_blk blocks; every block's rows lie in one statistics batch
 __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p, int rows_per_blk) {
   const int nch = p.C >> 3;
@@ -315,11 +316,26 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p
   const int rows_par = 256 / nchl;
   const int t = threadIdx.x;
   const int rl = t / nchl, cl = t - rl * nchl;
-  if (rl >= rows_par) return;
   const long long row0 = (long long)blockIdx.x * rows_per_blk;
   const int stat = (int)(row0 / p.rows_per_stat);
   const int cpg = p.C / p.G;
-  const double n = (double)cpg * p.rows_per_stat;
+  // per-group mean / rstd once per block (one fp64 divide + sqrt per group, not per channel and
+  // thread: the per-channel form spent more issue on fp64 divides and square roots than the
+  // block's 128 rows of streaming)
+  __shared__ float s_mean[GN_MAX_GROUPS], s_rstd[GN_MAX_GROUPS];
+  {
+    const double n = (double)cpg * p.rows_per_stat;
+    for (int g = t; g < p.G; g += 256) {
+      const double* acc = p.ws + ((size_t)stat * p.G + g) * 2;
+      const double mean = acc[0] / n;
+      double var = acc[1] / n - mean * mean;
+      if (var < 0.0) var = 0.0;
+      s_mean[g] = (float)mean;
+      s_rstd[g] = (float)(1.0 / sqrt(var + (double)p.eps));
+    }
+  }
+  __syncthreads();
+  if (rl >= rows_par) return;
   float sa[2][8], sb[2][8];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -328,13 +344,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = ch * 8 + e, g = c / cpg;
-        const double* acc = p.ws + ((size_t)stat * p.G + g) * 2;
-        const double mean = acc[0] / n;
-        double var = acc[1] / n - mean * mean;
-        if (var < 0.0) var = 0.0;
-        const float rstd = (float)(1.0 / sqrt(var + (double)p.eps));
-        sa[k][e] = rstd * p.gamma[c];
-        sb[k][e] = p.beta[c] - (float)mean * sa[k][e];
+        sa[k][e] = s_rstd[g] * p.gamma[c];
+        sb[k][e] = p.beta[c] - s_mean[g] * sa[k][e];
       }
     }
   }
@@ -374,6 +385,7 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   if (d->M % d->rows_per_stat) return ACTH_EINVAL;
   if (d->C1 < d->C && (!d->x2 || d->ldx2 % 8)) return ACTH_EINVAL;
   if (d->ldx % 8 || d->ldy % 8 || d->C > 4096 || d->silu < 0 || d->silu > 2) return ACTH_EINVAL;
+  if (d->G > GN_MAX_GROUPS) return ACTH_EINVAL;
   if (d->res && d->ldres % 8) return ACTH_EINVAL;
   const int nstat = d->M / d->rows_per_stat;
   if (nstat == 0) return ACTH_OK;

@@ -211,11 +211,11 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
 // ------------------------------------------------------------------------------------------
 // Single-pass scan with the 16 states of a channel split over a lane pair: lane 2c + j owns
 // states [8j, 8j+8) of channel c. Twice the parallelism of one-thread-per-channel (2240 waves at
-// ACTalker's level-0 shape) without the two-pass chunk decomposition: per token a lane does half
-// of the dt_proj dot product (partner's half arrives by a DPP swap), the softplus, 8 state updates
-// and half of the C readout (summed by a second swap). Tiles of SC_T tokens of xdbl / u are staged
-// in LDS (next tile prefetched into registers); outputs are gathered per tile in LDS and stored
-// with 16-byte coalesced writes.
+// ACTalker's level-0 shape) without the two-pass chunk decomposition: per token a lane reads the
+// token's delta (computed per tile on the matrix core, below), does 8 state updates and half of
+// the C readout (summed by a DPP swap). Tiles of SC_T tokens of xdbl / u are staged in LDS (next
+// tile prefetched into registers); outputs are gathered per tile in LDS and stored with 16-byte
+// coalesced writes.
 
 // softplus with the log taken by the raw v_log_f32 (log2): its argument 1 + exp(-|x|) lies in
 // [1, 2], so ocml's denormal range reduction around __logf is dead weight
@@ -230,20 +230,33 @@ __device__ __forceinline__ float pair_swap(float v) {
 }
 
 // CH channels per block (2 CH threads).
+//
+// dt_proj (R > 0) runs on the matrix core: per tile, each wave computes delta for its own 32
+// channels x SC_T tokens as two v_mfma_f32_16x16x4_f32 products (fp32 in, fp32 out: bitwise an fmaf
+// chain, no reduced precision), adds dt_bias and applies the softplus once per (token, channel) in
+// the accumulator layout, and parks the result in LDS (`dls`, the same slot the explicit-delta mode
+// stages). The recurrence lanes then read delta with one ds_read: the per-token VALU dot product
+// (R/2 packed FMAs per lane), its pair reduction and the softplus that both lanes of a pair used to
+// repeat leave the serial loop.
 template <int R, int CH, bool SOFTPLUS>
-__global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p) {
+__global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(const ActhScanDesc p) {
   constexpr int NT = 2 * CH;                     // threads
   constexpr int SP_CH = CH;
   constexpr int U16 = CH / 8;                    // 16-byte chunks per token row of the u / y tile
   constexpr int W = R + 32;                      // floats per token and group in xdbl
-  constexpr int R0 = (R + 1) / 2;                // dt_proj terms of lane half 0 (half 1 takes R - R0)
-  constexpr int R0P = (R0 + 3) & ~3;             // each half's dt slice, 16-byte aligned, zero padded
-  constexpr int WP = 2 * R0P + 32;               // LDS row: [dt half 0 | dt half 1 | B | C]
+  constexpr int R4 = (R + 3) & ~3;               // dt columns padded to whole 16x16x4 k-steps
+  constexpr int KS = R4 / 4;                     // k-steps per lane group (group g holds k = g*KS + s)
+  constexpr int WP0 = R4 + 32;                   // LDS row: [dt (R4) | B | C]
+  constexpr int WP = ((WP0 / 4) % 2 == 0) ? WP0 + 4 : WP0;   // odd 16-byte stride: the MFMA B reads
+                                                              // of 16 token rows hit distinct banks
+  constexpr int DLP = SP_CH + 4;                 // delta tile row (padded: the 16 token rows of an
+                                                 // accumulator store land in different banks)
   constexpr int NX = (SC_T * W + NT - 1) / NT;
+  static_assert(CH % 32 == 0, "a wave owns 32 channels");
   __shared__ __attribute__((aligned(16))) float xs[SC_T * WP];
   __shared__ __attribute__((aligned(16))) bf16_t us[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) bf16_t ys[SC_T * SP_CH];
-  __shared__ __attribute__((aligned(16))) float dls[R == 0 ? SC_T * SP_CH : 4];
+  __shared__ __attribute__((aligned(16))) float dls[SC_T * DLP];
 
   const int k = blockIdx.y, b = blockIdx.z;
   const int t = threadIdx.x;
@@ -254,22 +267,33 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
   const int dd = active ? d : 0;
   const bool rev = (k == 1) && p.flip1;
 
-  // dt_proj weights of this lane's half as pairs (packed FMAs: two products per v_pk_fma_f32)
-  f32x2_t w2[R0P > 0 ? R0P / 2 : 1];
+  // dt_proj on MFMA: lane (g = lane >> 4, i = lane & 15) of wave w supplies A = dt_w[channel
+  // 32 w + 16 mb + i][g KS + s] and B = xdbl_dt[token i][g KS + s]; its accumulator rows are the
+  // channels 32 w + 16 mb + 4 g + r, column token i
+  const int ln = t & 63, wv = t >> 6, mg = ln >> 4, mi = ln & 15;
+  float wa[2][R > 0 ? KS : 1], bo[2][4];
 #pragma unroll
-  for (int r = 0; r < R0P; ++r) {
-    const int rr = half ? R0 + r : r;
-    w2[r / 2][r % 2] = (r < R0 && rr < R) ? p.dt_w[((size_t)k * p.D + dd) * R + rr] : 0.0f;
-  }
-  // zero the dt padding columns once (commit() never writes them; they meet zero weights)
-  if (R > 0) {
-    for (int idx = t; idx < SC_T * 2 * R0P; idx += NT) {
-      const int tt = idx / (2 * R0P), c = idx - tt * (2 * R0P);
-      const int hf = c / R0P, r = c - hf * R0P;
-      if (r >= (hf ? R - R0 : R0)) xs[tt * WP + c] = 0.0f;
+  for (int mb = 0; mb < 2; ++mb) {
+    const int ch = dbase + 32 * wv + 16 * mb + mi;
+#pragma unroll
+    for (int s = 0; s < (R > 0 ? KS : 1); ++s) {
+      const int r = mg * KS + s;
+      wa[mb][s] = (R > 0 && r < R && ch < p.D) ? p.dt_w[((size_t)k * p.D + ch) * R + r] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = dbase + 32 * wv + 16 * mb + 4 * mg + r;
+      bo[mb][r] = (p.dt_b && co < p.D) ? p.dt_b[k * p.D + co] : 0.0f;
     }
   }
-  const float bias = p.dt_b ? p.dt_b[k * p.D + dd] : 0.0f;
+  // zero the dt padding columns once (commit() never writes them; they meet zero weights)
+  if (R4 > R) {
+    for (int idx = t; idx < SC_T * (R4 - R); idx += NT) {
+      const int tt = idx / (R4 - R), c = idx - tt * (R4 - R);
+      xs[tt * WP + R + c] = 0.0f;
+    }
+  }
+  const float bias = p.dt_b ? p.dt_b[k * p.D + dd] : 0.0f;   // explicit-delta mode only
   // this lane's 8 states as 4 pairs: A * log2(e) and h
   f32x2_t a2[4], h[4];
 #pragma unroll
@@ -330,8 +354,7 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
       const int idx = t + e * NT;
       if (idx < SC_T * W) {
         const int tt = idx / W, col = idx - tt * W;
-        const int dst = col < R0 ? col : col < R ? R0P + (col - R0) : 2 * R0P + (col - R);
-        xs[tt * WP + dst] = px[e];
+        xs[tt * WP + (col < R ? col : col - R + R4)] = px[e];
       }
     }
     *reinterpret_cast<uint4*>(&us[(t / U16) * SP_CH + (t % U16) * 8]) = pu;
@@ -339,8 +362,43 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int idx = t + e * NT;
-        *reinterpret_cast<float4*>(&dls[(idx / (CH / 4)) * SP_CH + (idx % (CH / 4)) * 4]) = pd[e];
+        *reinterpret_cast<float4*>(&dls[(idx / (CH / 4)) * DLP + (idx % (CH / 4)) * 4]) = pd[e];
       }
+    }
+  };
+  // delta of the committed tile for this wave's 32 channels (R > 0): dt_proj on the matrix core,
+  // + dt_bias, softplus, into dls[token][channel]. Wave-local: the recurrence lanes that read a
+  // channel's delta belong to the wave that wrote it (LDS ops of one wave complete in order).
+  auto delta_tile = [&]() {
+    if constexpr (R > 0) {
+      f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float bv = xs[mi * WP + mg * KS + s];
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][s], bv, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[1][s], bv, acc[1], 0, 0, 0);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        float4 o;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = acc[mb][r] + bo[mb][r];
+          v[r] = SOFTPLUS ? softplus_raw(x) : x;
+        }
+        o = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(&dls[mi * DLP + 32 * wv + 16 * mb + 4 * mg]) = o;
+      }
+    }
+  };
+  // delta of token tt for this lane's channel (softplus applied)
+  auto dt_of = [&](int tt) {
+    if constexpr (R == 0) {
+      const float x = dls[tt * DLP + cl] + bias;
+      return SOFTPLUS ? softplus_raw(x) : x;
+    } else {
+      return dls[tt * DLP + cl];
     }
   };
 
@@ -349,31 +407,16 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
     commit();
     __syncthreads();
     if (i0 + SC_T < p.L) prefetch(i0 + SC_T);
+    delta_tile();
     const int nt = min(SC_T, p.L - i0);
-    // one token of the recurrence; full tiles are unrolled so the dt / exp work of later tokens
-    // (independent of h) overlaps the serial state updates
+    // one token of the recurrence (partial last tile)
     auto token = [&](int tt) {
       const float* xr = xs + tt * WP;
-      float dt;
-      if constexpr (R == 0) {
-        dt = dls[tt * SP_CH + cl] + bias;
-      } else {
-        const float4* xr4 = reinterpret_cast<const float4*>(xr + half * R0P);
-        f32x2_t part = {0.0f, 0.0f};
-#pragma unroll
-        for (int r4 = 0; r4 < R0P / 4; ++r4) {
-          const float4 v = xr4[r4];
-          part = __builtin_elementwise_fma(w2[2 * r4], (f32x2_t){v.x, v.y}, part);
-          part = __builtin_elementwise_fma(w2[2 * r4 + 1], (f32x2_t){v.z, v.w}, part);
-        }
-        const float ph = part.x + part.y;
-        dt = ph + pair_swap(ph) + bias;
-      }
-      if (SOFTPLUS) dt = softplus_raw(dt);
+      const float dt = dt_of(tt);
       const float uu = bf2f(us[tt * SP_CH + cl]);
       const float du = dt * uu;
-      const float4* bv = reinterpret_cast<const float4*>(xr + 2 * R0P + 8 * half);
-      const float4* cv = reinterpret_cast<const float4*>(xr + 2 * R0P + 16 + 8 * half);
+      const float4* bv = reinterpret_cast<const float4*>(xr + R4 + 8 * half);
+      const float4* cv = reinterpret_cast<const float4*>(xr + R4 + 16 + 8 * half);
       const float4 b0 = bv[0], b1 = bv[1], c0 = cv[0], c1 = cv[1];
       const f32x2_t bb[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
       const f32x2_t cc[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
@@ -395,38 +438,18 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
     };
     if (nt == SC_T) {
       // Full tile, software-pipelined by hand (the compiler schedules each token's dependency chain
-      // on its own): (1) dt = softplus(dt_proj) and u of all SC_T tokens -- independent of the state;
-      // (2) the recurrence, with token tt+1's decays exp(dt A) and inputs dt u B computed before
-      // token tt's state update so their latency hides under it.
-      float dtv[SC_T], uuv[SC_T];
-#pragma unroll
-      for (int tt = 0; tt < SC_T; ++tt) {
-        const float* xr = xs + tt * WP;
-        float dt;
-        if constexpr (R == 0) {
-          dt = dls[tt * SP_CH + cl] + bias;
-        } else {
-          const float4* xr4 = reinterpret_cast<const float4*>(xr + half * R0P);
-          f32x2_t part = {0.0f, 0.0f};
-#pragma unroll
-          for (int r4 = 0; r4 < R0P / 4; ++r4) {
-            const float4 v = xr4[r4];
-            part = __builtin_elementwise_fma(w2[2 * r4], (f32x2_t){v.x, v.y}, part);
-            part = __builtin_elementwise_fma(w2[2 * r4 + 1], (f32x2_t){v.z, v.w}, part);
-          }
-          const float ph = part.x + part.y;
-          dt = ph + pair_swap(ph) + bias;
-        }
-        dtv[tt] = SOFTPLUS ? softplus_raw(dt) : dt;
-        uuv[tt] = bf2f(us[tt * SP_CH + cl]);
-      }
+      // on its own): token tt+1's delta / u reads, decays exp(dt A) and inputs dt u B are computed
+      // before token tt's state update so their latency hides under it.
       f32x2_t ee[2][4], db[2][4];
+      float uus[2];
       auto prep = [&](int tt, int slot) {
         const float* xr = xs + tt * WP;
-        const float4* bv = reinterpret_cast<const float4*>(xr + 2 * R0P + 8 * half);
+        const float4* bv = reinterpret_cast<const float4*>(xr + R4 + 8 * half);
         const float4 b0 = bv[0], b1 = bv[1];
         const f32x2_t bb[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
-        const float dt = dtv[tt], du = dt * uuv[tt];
+        const float uu = bf2f(us[tt * SP_CH + cl]);
+        const float dt = dt_of(tt), du = dt * uu;
+        uus[slot] = uu;
         const f32x2_t dt2 = {dt, dt}, du2 = {du, du};
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
@@ -440,7 +463,7 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
       for (int tt = 0; tt < SC_T; ++tt) {
         if (tt + 1 < SC_T) prep(tt + 1, (tt + 1) & 1);
         const float* xr = xs + tt * WP;
-        const float4* cv = reinterpret_cast<const float4*>(xr + 2 * R0P + 16 + 8 * half);
+        const float4* cv = reinterpret_cast<const float4*>(xr + R4 + 16 + 8 * half);
         const float4 c0 = cv[0], c1 = cv[1];
         const f32x2_t cc[4] = {{c0.x, c0.y}, {c0.z, c0.w}, {c1.x, c1.y}, {c1.z, c1.w}};
         f32x2_t y2 = {0.0f, 0.0f};
@@ -451,7 +474,7 @@ __global__ __launch_bounds__(2 * CH) void scan_pair_kernel(const ActhScanDesc p)
         }
         float y = y2.x + y2.y;
         y += pair_swap(y);
-        ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uuv[tt], y));
+        ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uus[tt & 1], y));
       }
     } else {
       for (int tt = 0; tt < nt; ++tt) token(tt);

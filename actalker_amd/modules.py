@@ -122,6 +122,16 @@ class Ctx:
         self.audio_zero = False     # gate hints: tokens known to be exactly zero
         self.vasa_zero = False
         self.has_ip = True
+        self.tproj = {}             # id(ResBlock) -> its time_emb_proj(temb) (B, C) f32 view (batched GEMM)
+        self.vid = {}               # id(attn2) -> its to_v(ID token) (rows, C) bf16 view (batched GEMM)
+        self.ipkv = {}              # id(attn2) -> IP audio K|V (rows, 2C) view (batched GEMM)
+        self.ipvb = {}              # id(attn2) -> IP VASA V (rows, C) view (batched GEMM)
+
+    def temb_proj(self, blk):
+        tp = self.tproj.get(id(blk))
+        if tp is None:
+            tp = ops.gemm(self.temb, blk.time_emb_proj.w(), bias=blk.time_emb_proj.b(), out_f32=True)
+        return tp
 
     def mask(self, k: int, S: int):
         if self.masks is None:
@@ -233,7 +243,7 @@ class ResnetBlock2D(nn.Module):
         S = H * W
         g1, b1 = self.norm1.gb()
         n1 = ops.groupnorm(x, g1, b1, self.norm1.eps, S, x2=x2, silu=True)
-        tp = ops.gemm(ctx.temb, self.time_emb_proj.w(), bias=self.time_emb_proj.b(), out_f32=True)
+        tp = ctx.temb_proj(self)
         h = ops.conv3x3(n1, self.conv1.w3(), ctx.BF, H, W, bias=self.conv1.b(), rowbias=tp, rb_div=ctx.F * S)
         del n1
         g2, b2 = self.norm2.gb()
@@ -265,7 +275,7 @@ class TemporalResnetBlock(nn.Module):
         FS = ctx.F * S
         g1, b1 = self.norm1.gb()
         n1 = ops.groupnorm(x, g1, b1, self.norm1.eps, FS, silu=True)
-        tp = ops.gemm(ctx.temb, self.time_emb_proj.w(), bias=self.time_emb_proj.b(), out_f32=True)
+        tp = ctx.temb_proj(self)
         t = ops.gemm(n1, self.conv1.wt(), temporal=dict(F=ctx.F, S=S), bias=self.conv1.b(), rowbias=tp, rb_div=FS)
         del n1
         g2, b2 = self.norm2.gb()
@@ -421,16 +431,22 @@ class Attention(Packed):
             use_a = not ctx.audio_zero and not (ia is not None and ia.all_zero)
             use_b = not ctx.vasa_zero and not (ib is not None and ib.all_zero)
         # softmax over a single key is exactly 1: the ID attention is to_v(ID) broadcast
-        v_id = ops.gemm(id_tok, self.to_v.w())
+        v_id = ctx.vid.get(id(self))
+        if v_id is None or v_id.shape[0] != id_tok.shape[0]:
+            v_id = ops.gemm(id_tok, self.to_v.w())
         proc = self.processor
         if is_ip_processor(proc):
             sa, sb = _scale_value(proc.scale[0]), _scale_value(proc.scale[1])
             q = kv = vb = None
             if use_a and sa != 0.0:
                 q = ops.gemm(n, self.to_q.w())
-                kv = ops.gemm(audio, ip_w_kv(proc, 0))
+                kv = ctx.ipkv.get(id(self))                    # batched per call (UNet._batched_ctx_projections)
+                if kv is None or kv.shape[0] != audio.shape[0]:
+                    kv = ops.gemm(audio, ip_w_kv(proc, 0))
             if use_b and sb != 0.0:
-                vb = ops.gemm(vasa, ip_w_v(proc, 1))
+                vb = ctx.ipvb.get(id(self))
+                if vb is None or vb.shape[0] != vasa.shape[0]:
+                    vb = ops.gemm(vasa, ip_w_v(proc, 1))
             comb = ops.ip_attn(v_id, M, self.heads, rows_per_ctx, S, q=q, kv=kv, nkeys=ctx.n_audio, vb=vb,
                                mask_a=ma, mask_b=mb, sa=sa, sb=sb)
         else:
@@ -682,9 +698,18 @@ class TransformerSpatioTemporalModel(nn.Module):
         pass
 
     def _pos_emb(self, ctx: Ctx):
-        """time_pos_embed(Timesteps(C)(frame index)) for frames 0..F-1 of every batch element: (BF, C)."""
-        fidx = torch.arange(ctx.F, device=ctx.device, dtype=torch.float32).repeat(ctx.B)
-        return self.time_pos_embed.run(self.time_proj.run(fidx))
+        """time_pos_embed(Timesteps(C)(frame index)) for frames 0..F-1 of every batch element: (BF, C).
+        A function of the weights and (B, F) only -- the same in every UNet call of a run -- so it is
+        cached, keyed on the TimestepEmbedding tensors' versions (two 84-row GEMMs per transformer and
+        call otherwise)."""
+        te = self.time_pos_embed
+        tensors = [t for t in (te.linear_1.weight, te.linear_1.bias, te.linear_2.weight, te.linear_2.bias)
+                   if t is not None]
+
+        def make():
+            fidx = torch.arange(ctx.F, device=ctx.device, dtype=torch.float32).repeat(ctx.B)
+            return te.run(self.time_proj.run(fidx))
+        return _versioned_pack(self, ("pos_emb", ctx.B, ctx.F, str(ctx.device)), tensors, make)
 
     def run(self, ctx: Ctx, x, H, W, prefix=None):
         """``prefix`` = (ctx_u, expand): ``x`` holds only the batch elements of ``ctx_u`` (the distinct

@@ -21,7 +21,7 @@ from typing import Sequence, Any, Dict, List, Optional, Tuple, Union
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import modules, ops
 from .modules import (Attention, AttnProcessor2_0, Conv2d, CrossAttnDownBlockSpatioTemporal,
                       CrossAttnUpBlockSpatioTemporal, Ctx, DownBlockSpatioTemporal, GroupNorm,
                       IPAdapterAttnProcessor2_0, Timesteps, TimestepEmbedding,
@@ -298,12 +298,83 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         else:
             ctx.has_ip = False
         ctx.id_mean = ops.frame_mean(ctx.id_tok, B, F, 1)
+        self._batched_ctx_projections(ctx)
         cak = cross_attention_kwargs or {}
         ctx.masks = cak.get("ip_adapter_masks")
         gate = cak.get("acth_gate")       # optional hint from actalker_amd.pipeline: exact-zero branches
         if gate is not None:
             ctx.audio_zero, ctx.vasa_zero = gate[0] == 0, gate[1] == 0
         return ctx
+
+    def _batched_ctx_projections(self, ctx):
+        """The per-call inputs every ResBlock / cross attention projects on its own -- ``temb`` through
+        each ResBlock's ``time_emb_proj`` (diffusers resnet.py: ~40 per call), the ID token through each
+        attn2's ``to_v`` (16 spatial on ``id_tok``, 16 temporal on ``id_mean``) -- as three GEMMs over the
+        concatenated weights, once per UNet call. Each of the ~70 separate products is a 6- or 84-row GEMM
+        that fills 3-10 workgroups for ~25-30 us; the results are column views handed to the modules
+        (``ctx.tproj`` / ``ctx.vid``), which fall back to their own GEMM when absent."""
+        if not getattr(self, "acth_batch_ctx_projections", True):
+            return
+        mods = self.__dict__.get("_acth_ctx_mods")
+        if mods is None:                     # module lists, walked once (the tree is fixed after __init__)
+            res, sp, tp = [], [], []
+            for m in self.modules():
+                if isinstance(m, (modules.ResnetBlock2D, modules.TemporalResnetBlock)) and m.time_emb_proj is not None:
+                    res.append(m)
+                elif isinstance(m, modules.TransformerSpatioTemporalModel):
+                    sp += [blk.attn2 for blk in m.transformer_blocks]
+                    tp += [blk.attn2 for blk in m.temporal_transformer_blocks]
+            mods = self.__dict__["_acth_ctx_mods"] = (res, sp, tp)
+        res, sp, tp = mods
+        if res:
+            lins = [m.time_emb_proj for m in res]
+            tensors = [t for l in lins for t in ((l.weight, l.bias) if l.bias is not None else (l.weight,))]
+
+            def pack_t():
+                w = modules._bf(torch.cat([l.weight for l in lins], 0))
+                b = torch.cat([l.bias if l.bias is not None else torch.zeros(l.out_features, device=l.weight.device)
+                               for l in lins]).float().contiguous()
+                return w, b
+            w, b = modules._versioned_pack(self, "temb_all", tensors, pack_t)
+            out = ops.gemm(ctx.temb, w, bias=b, out_f32=True)
+            ctx.tproj, o = {}, 0
+            for m, l in zip(res, lins):
+                ctx.tproj[id(m)] = out[:, o:o + l.out_features]
+                o += l.out_features
+        # IP-adapter audio K|V (to_k_ip[0] | to_v_ip[0]) and VASA V (to_v_ip[1]) of every IP attn2, on the
+        # frame tokens (spatial) or the window means (temporal): the same concatenation
+        ctx.ipkv, ctx.ipvb = {}, {}
+        if ctx.has_ip:
+            for key, attns, atok, vtok in (("s", sp, ctx.audio_tok, ctx.vasa_tok),
+                                           ("t", tp, ctx.audio_mean, ctx.vasa_mean)):
+                procs = [(a, a.processor) for a in attns if modules.is_ip_processor(a.processor)]
+                if not procs:
+                    continue
+                for dst, zero, tok, srcs in (
+                        (ctx.ipkv, ctx.audio_zero, atok, [(pr.to_k_ip[0].weight, pr.to_v_ip[0].weight) for _, pr in procs]),
+                        (ctx.ipvb, ctx.vasa_zero, vtok, [(pr.to_v_ip[1].weight,) for _, pr in procs])):
+                    if zero or tok is None:
+                        continue
+                    flat = [t for ws in srcs for t in ws]
+                    w = modules._versioned_pack(self, ("ip", key, len(srcs[0])), flat,
+                                                lambda flat=flat: modules._bf(torch.cat(flat, 0)))
+                    out = ops.gemm(tok, w)
+                    o = 0
+                    for (a, _), ws in zip(procs, srcs):
+                        n = sum(t.shape[0] for t in ws)
+                        dst[id(a)] = out[:, o:o + n]
+                        o += n
+        ctx.vid = {}
+        for key, attns, tok in (("vid_s", sp, ctx.id_tok), ("vid_t", tp, ctx.id_mean)):
+            if not attns:
+                continue
+            ws = [a.to_v.weight for a in attns]
+            w = modules._versioned_pack(self, key, ws, lambda ws=ws: modules._bf(torch.cat(ws, 0)))
+            out = ops.gemm(tok, w)
+            o = 0
+            for a, wt in zip(attns, ws):
+                ctx.vid[id(a)] = out[:, o:o + wt.shape[0]]
+                o += wt.shape[0]
 
     def forward_tokens(self, x_tok: torch.Tensor, B: int, F: int, H: int, W: int, timestep, encoder_hidden_states,
                        added_time_ids, spatial_condition_tok: Optional[torch.Tensor] = None,

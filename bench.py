@@ -326,6 +326,8 @@ def main():
     ap.add_argument("--no-share-prefix", action="store_true",
                     help="run the UNet prefix before the first IP-adapter input for every CFG branch (no sharing "
                          "between the branches whose prefix inputs are equal)")
+    ap.add_argument("--no-batch-ctx-proj", action="store_true",
+                    help="per-module time_emb_proj / to_v(ID) GEMMs instead of the three batched ones per UNet call")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
     ap.add_argument("--no-four-branch-compare", action="store_true",
@@ -358,6 +360,7 @@ def main():
     t0 = time.time()
     unet_cpu = build_unet(dev)
     unet = unet_cpu.to(dev)
+    unet.acth_batch_ctx_projections = not args.no_batch_ctx_proj
     log(f"model built in {time.time() - t0:.1f}s")
     inp = synthetic_inputs(N, fpb, H, W, args.mode)
     backend = pl.HipBackend(unet, H // 8, W // 8, inp["masks"], gate, inp["added"], N + fpb, fpb,
@@ -404,7 +407,7 @@ def main():
     if timer is not None and timer.launches:
         gemm_ms = timer.total_ms()
         if os.environ.get("ACTH_GEMM_STATS"):
-            log(timer.shape_report())
+            log(timer.shape_report(top=int(os.environ.get("ACTH_GEMM_STATS")) or 25))
         achieved = timer.flops / (gemm_ms / 1000.0) / 1e12
         pmc = pmc_traffic()
         roof = dict(bound="mfma", achieved=round(achieved, 2), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",

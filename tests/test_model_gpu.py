@@ -168,6 +168,30 @@ def test_cfg_prefix_sharing_matches_full_batch(dev, tiny):
         unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak, prefix_src=[0, 2, 2])
 
 
+def test_batched_ctx_projections_match_per_module(dev, tiny):
+    """UNet._batched_ctx_projections: every ResBlock's time_emb_proj(temb) and every attn2's to_v(ID token)
+    computed as three concatenated-weight GEMMs per call == the per-module GEMMs (only the GEMM tile
+    choice for the wider N may differ), with the prefix-sharing context too."""
+    from actalker_amd import ops
+    unet, sd, cfg = tiny
+    sample, t, ehs, added, pose, masks = ge._tiny_inputs(B=3, F=3, H=16, W=32, seed=9)
+    B, F, H, W = 3, 3, 16, 32
+    x = ops.nchw_to_tokens(sample.to(dev))
+    sc = ops.nchw_to_tokens(pose.to(dev))
+    e = (ehs[0].to(dev), [a.to(dev) for a in ehs[1]])
+    cak = {"ip_adapter_masks": masks}
+    try:
+        with torch.no_grad():
+            unet.acth_batch_ctx_projections = True
+            batched = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak)
+            unet.acth_batch_ctx_projections = False
+            single = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak)
+    finally:
+        unet.acth_batch_ctx_projections = True
+    assert torch.isfinite(batched.float()).all()
+    assert rel(batched, single) < 1e-3
+
+
 def test_pipeline_prefix_sharing_matches_unshared_loop(dev, tiny):
     """The sampler loop with LoopConfig.share_cfg_prefix on and off, CFG inputs shaped as the reference
     builds them (pipeline:162-205: branch 0 zero image latents / ID, branches 1-3 equal image latents;

@@ -194,12 +194,20 @@ static double tile_eff(long long mt, int N, int bn) {
 
 static int choose_tile(const ActhGemmDesc* d) {
   if (d->tile & 0xff) return d->tile & 0xff;
+  // Tall-skinny, HBM-bound on A (>= 128 row tiles; the Mamba x_proj, N = 2 (R + 32) = 104 / 144 / 224,
+  // and the UNet conv_out, N = 4): the phased kernels stream A through LDS-DMA whatever the column
+  // padding costs. Measured (tools/bench_gemm.py, profiles/r2_step19_bench_gemm_tall_skinny.log):
+  // 776916x104x640 311 -> 374 TF/s (256x128), 196308x144x1280 451 -> 516 and 51156x224x2560
+  // 382 -> 773 (256x256 instead of 256x160), conv 774144x4x2880 17.7 -> 21.4.
+  const bool tall = d->act != 2 && d->M >= 256 * 128;
+  if (tall && d->N < 128) return 6;
   if (d->N < 128 || d->M < 256) return 1;
   const long long mt = (d->M + 255) / 256;
   if (d->act == 2) return (d->N % 256 == 0 && mt * (d->N / 256) >= 192) ? 4 : 1;
   const double e5 = tile_eff(mt, d->N, 320), e4 = tile_eff(mt, d->N, 256);
   if (e5 >= 0.7 && e5 >= e4) return 5;
   if (e4 >= 0.7) return 4;
+  if (tall && d->N > 128 && d->N <= 256) return 4;
   return 3;
 }
 
@@ -275,7 +283,7 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   if (b_bytes >= 0x80000000LL) return ACTH_EINVAL;
   if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL) return gemm_split_rows(d, stream);
   const int tile = choose_tile(d) & 0xff;
-  if (tile == 4 || tile == 5)
+  if (tile == 4 || tile == 5 || tile == 6)
     return gemm8p_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
   if (tile == 2 || tile == 3)
     return gemm256_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);

@@ -600,7 +600,8 @@ static int gemm8p_group_m(const ActhGemmDesc* d) {
   return (long long)d->N * d->K * 2 > (4ll << 20) ? 8 : 0;
 }
 
-// tile 4: 256 x 256; tile 5: 256 x 320 (no GEGLU: its wave column shares are not granule pairs)
+// tile 4: 256 x 256; tile 5: 256 x 320; tile 6: 256 x 128 (the tall-skinny Mamba x_proj: N = 104 on
+// 776916 rows, HBM-bound on A). Tiles 5 / 6: no GEGLU (wave column shares are not granule pairs).
 int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                   int vec_ok, hipStream_t stream) {
   const int mt = (d->M + 255) / 256;
@@ -611,6 +612,8 @@ int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2
     launch8p<256>(&dd, dim3((d->N + 255) / 256, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
   } else if (tile == 5 && d->act != 2) {
     launch8p<320>(&dd, dim3((d->N + 319) / 320, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+  } else if (tile == 6 && d->act != 2) {
+    launch8p<128>(&dd, dim3((d->N + 127) / 128, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
   } else {
     return ACTH_EINVAL;
   }

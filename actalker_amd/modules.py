@@ -126,6 +126,7 @@ class Ctx:
         self.vid = {}               # id(attn2) -> its to_v(ID token) (rows, C) bf16 view (batched GEMM)
         self.ipkv = {}              # id(attn2) -> IP audio K|V (rows, 2C) view (batched GEMM)
         self.ipvb = {}              # id(attn2) -> IP VASA V (rows, C) view (batched GEMM)
+        self.mamba_proj = {}        # id(Mamba id / audio / exp Linear) -> SiLU(tokens @ W^T) view (batched)
 
     def temb_proj(self, blk):
         tp = self.tproj.get(id(blk))
@@ -646,8 +647,17 @@ class SS2D_cond_v10(nn.Module):
             xz = ops.gemm(h, in_proj.w())
             ops.gather_rows(xz, info.idx, BF, S, u, L)
             br.update(mode=2, x=xz, pos=info.pos)
-        ops.gemm(ctx.id_tok, self.id_proj.w(), act=ops.ACT_SILU, out=u, orow=(1, L, n_sel))
-        ops.gemm(cond_tok, cond_proj.w(), act=ops.ACT_SILU, out=u, orow=(n_cond, L, n_sel + 1))
+        uv = u.view(BF, L, Din)
+        idp = ctx.mamba_proj.get(id(self.id_proj))            # batched per call (UNet._batched_ctx_projections)
+        if idp is not None and idp.shape[0] == BF:
+            uv[:, n_sel].copy_(idp)
+        else:
+            ops.gemm(ctx.id_tok, self.id_proj.w(), act=ops.ACT_SILU, out=u, orow=(1, L, n_sel))
+        cp = ctx.mamba_proj.get(id(cond_proj))
+        if cp is not None and cp.shape[0] == cond_tok.shape[0]:
+            uv[:, n_sel + 1:n_sel + 1 + n_cond].copy_(cp.view(BF, n_cond, Din))
+        else:
+            ops.gemm(cond_tok, cond_proj.w(), act=ops.ACT_SILU, out=u, orow=(n_cond, L, n_sel + 1))
         br["y0"], br["y1"] = unit.scan(u, BF, L, n_sel)
         br["L"] = n_sel          # scan outputs hold n_sel rows per batch element
         return br

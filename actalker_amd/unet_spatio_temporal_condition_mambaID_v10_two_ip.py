@@ -298,12 +298,12 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         else:
             ctx.has_ip = False
         ctx.id_mean = ops.frame_mean(ctx.id_tok, B, F, 1)
-        self._batched_ctx_projections(ctx)
         cak = cross_attention_kwargs or {}
         ctx.masks = cak.get("ip_adapter_masks")
         gate = cak.get("acth_gate")       # optional hint from actalker_amd.pipeline: exact-zero branches
         if gate is not None:
             ctx.audio_zero, ctx.vasa_zero = gate[0] == 0, gate[1] == 0
+        self._batched_ctx_projections(ctx)
         return ctx
 
     def _batched_ctx_projections(self, ctx):
@@ -317,15 +317,33 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             return
         mods = self.__dict__.get("_acth_ctx_mods")
         if mods is None:                     # module lists, walked once (the tree is fixed after __init__)
-            res, sp, tp = [], [], []
+            res, sp, tp, mb = [], [], [], []
             for m in self.modules():
                 if isinstance(m, (modules.ResnetBlock2D, modules.TemporalResnetBlock)) and m.time_emb_proj is not None:
                     res.append(m)
                 elif isinstance(m, modules.TransformerSpatioTemporalModel):
                     sp += [blk.attn2 for blk in m.transformer_blocks]
                     tp += [blk.attn2 for blk in m.temporal_transformer_blocks]
-            mods = self.__dict__["_acth_ctx_mods"] = (res, sp, tp)
-        res, sp, tp = mods
+                elif isinstance(m, modules.SS2D_cond_v10):
+                    mb.append(m)
+            mods = self.__dict__["_acth_ctx_mods"] = (res, sp, tp, mb)
+        res, sp, tp, mb = mods
+        # the Mamba blocks' SiLU(ID / audio / VASA token projections) (mamba_layer.py:1955-1960), the rows
+        # each branch places after its selected tokens: one GEMM per token kind, copied into place
+        ctx.mamba_proj = {}
+        if mb:
+            groups = [("id", [m.id_proj for m in mb], ctx.id_tok)]
+            if ctx.has_ip:
+                groups += [("audio", [m.audio_proj for m in mb], ctx.audio_tok),
+                           ("exp", [m.exp_proj for m in mb], ctx.vasa_tok)]
+            for key, lins, tok in groups:
+                ws = [l.weight for l in lins]
+                w = modules._versioned_pack(self, ("mamba", key), ws, lambda ws=ws: modules._bf(torch.cat(ws, 0)))
+                out = ops.gemm(tok, w, act=ops.ACT_SILU)
+                o = 0
+                for l in lins:
+                    ctx.mamba_proj[id(l)] = out[:, o:o + l.out_features]
+                    o += l.out_features
         if res:
             lins = [m.time_emb_proj for m in res]
             tensors = [t for l in lins for t in ((l.weight, l.bias) if l.bias is not None else (l.weight,))]

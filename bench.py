@@ -128,6 +128,7 @@ class GemmTimer:
 
     def __init__(self):
         self.events = []
+        self.work = []                 # (flop, algorithmic bytes) per launch, parallel to events
         self.flops = 0.0
         self.bytes = 0.0
         self.launches = 0
@@ -152,11 +153,13 @@ class GemmTimer:
                 M = kw["M"]
             else:
                 M = a.shape[0]
-            self.flops += 2.0 * M * N * K
-            self.bytes += gemm_algorithmic_bytes(a, w, M, N, K, kw)
+            fl, by = 2.0 * M * N * K, gemm_algorithmic_bytes(a, w, M, N, K, kw)
+            self.flops += fl
+            self.bytes += by
             self.launches += 1
             mode = "conv" if kw.get("conv") is not None else "temporal" if kw.get("temporal") is not None else "dense"
             self.events.append((e0, e1, (mode, M, N, K, kw.get("act", 0))))
+            self.work.append((fl, by))
             return out
         ops.gemm = timed
         import actalker_amd.modules as mods
@@ -169,6 +172,21 @@ class GemmTimer:
 
     def total_ms(self):
         return sum(a.elapsed_time(b) for a, b, _ in self.events)
+
+    def roofline_time(self):
+        """Per-launch roofline: each launch's floor is max(FLOP / MFMA peak, algorithmic bytes / HBM peak);
+        returns (sum of floors / sum of measured times, share of measured time in launches whose floor is
+        the HBM one). The small-K level-0 GEMMs (K = 320: 2 FLOP per byte of A read and C written) are
+        HBM-bound, which the family's single MFMA fraction does not show."""
+        t_floor = t_meas = t_hbm = 0.0
+        for (a, b, _), (fl, by) in zip(self.events, self.work):
+            ms = a.elapsed_time(b)
+            f_mfma, f_hbm = fl / (PEAK_BF16_TFLOPS * 1e9), by / (PEAK_HBM_GBS * 1e6)
+            t_floor += max(f_mfma, f_hbm)
+            t_meas += ms
+            if f_hbm > f_mfma:
+                t_hbm += ms
+        return (t_floor / t_meas if t_meas else None), (t_hbm / t_meas if t_meas else None)
 
     def shape_report(self, top=25):
         agg = {}
@@ -420,6 +438,12 @@ def main():
                     launches=timer.launches, avg_launch_us=round(1000.0 * gemm_ms / timer.launches, 2),
                     flop_per_launch=round(timer.flops / timer.launches),
                     kernel_share_of_step=round(gemm_ms / (elapsed * 1000.0), 3))
+        rt, hbm_share = timer.roofline_time()
+        if rt is not None:
+            roof["per_launch_roofline"] = dict(
+                time_frac=round(rt, 4), hbm_bound_time_share=round(hbm_share, 4),
+                definition="sum over GEMM launches of max(FLOP / 2500 TFLOP/s, algorithmic bytes / 8000 GB/s) "
+                           "divided by the sum of measured launch times")
     n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank, branches=branches)[0])
     frame_fwds = n_units_rank * fpb * args.steps
     # the reference-shaped figure: all four CFG branches evaluated (no twin-branch elimination), same steps

@@ -227,10 +227,10 @@ def test_gemm_host_bounds_checks(dev):
         ops.gemm(a, w, out=torch.empty(300, 128, device=dev, dtype=torch.bfloat16), orow=(100, 110, 0))
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
 def test_gemm_tile_variants(dev, tile):
-    """Every tile kernel (128x128; 256x256 / 256x160 8-wave; phased 256x256 / 256x320) on all A
-    loaders, tails and epilogues."""
+    """Every tile kernel (128x128; 256x256 / 256x160 8-wave; phased 256x256 / 256x320 / 256x128) on all
+    A loaders, tails and epilogues."""
     from actalker_amd.modules import pack_conv3x3, pack_conv3d_t, pack_geglu
     # dense, ragged M/N/K + bias + residual + silu, fp32 out
     M, N, K = 700, 330, 200
@@ -281,13 +281,23 @@ def test_gemm_tile_variants(dev, tile):
     xg = bf(rnd(Mg, Cg))
     wg, bg = rnd(2 * inner, Cg, scale=Cg ** -0.5), rnd(2 * inner, scale=0.1)
     wp, bp = pack_geglu(wg, bg)
-    if tile in (3, 5):
+    if tile in (3, 5, 6):
         with pytest.raises(Exception):
             ops.gemm(xg.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile)
     else:
         out = ops.gemm(xg.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile)
         h, g = (xg.float() @ bf(wg).float().t() + bg).chunk(2, -1)
         assert rel(out, h * F.gelu(g)) < 1e-2
+
+
+def test_gemm_tall_skinny_auto_tile(dev):
+    """The Mamba x_proj shape class (N = 2 (R + 32) <= 128 over >= 65536 rows, fp32 out) auto-selects
+    the phased 256x128 kernel; ragged last row tile, N not a multiple of 16."""
+    M, N, K = 256 * 260 - 37, 104, 640
+    a, w = bf(rnd(M, K)), bf(rnd(N, K, scale=K ** -0.5))
+    out = ops.gemm(a.to(dev), w.to(dev), out_f32=True)
+    assert out.dtype == torch.float32
+    assert rel(out, a.float() @ w.float().t()) < 1e-2
 
 
 @pytest.mark.parametrize("B,H,W,C1,C2,Cout,mode", [

@@ -23,6 +23,9 @@ SHAPES = [
     # reference points (not UNet shapes): square 4096^3 / 8192^3 (operands L2 / MALL resident),
     # and a 2048-wide K = 4096 panel streaming a 1 GB A from HBM
     ("dense", 4096, 4096, 4096, 0), ("dense", 8192, 8192, 8192, 0), ("dense", 131072, 2048, 4096, 0),
+    # the Mamba x_proj at levels 0 / 1 / 2 (N = 2 (R + 32); fp32 out in the UNet)
+    ("dense", 776916, 104, 640, 0), ("dense", 196308, 144, 1280, 0), ("dense", 51156, 224, 2560, 0),
+    ("conv", 774144, 4, 2880, 0),        # conv_out
 ]
 CONV_HW = {774144: (72, 128), 193536: (36, 64), 48384: (18, 32), 12096: (9, 16),
            516096: (72, 128), 129024: (36, 64), 32256: (18, 32), 8064: (9, 16)}

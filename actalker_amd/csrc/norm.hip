@@ -231,9 +231,9 @@ __device__ __forceinline__ uint4 gn_load(const ActhGroupNormDesc& p, long long r
   return *reinterpret_cast<const uint4*>((const bf16_t*)p.x2 + row * p.ldx2 + (c - p.C1));
 }
 
-// grid: (ceil(rows_per_stat / gs_rows), nstat); gs_rows (rows per block) is the largest of
-// 128 / 256 / 512 that still gives >= 1024 blocks: the per-block fold below is serial, so fewer,
-// fuller blocks keep the pass streaming (128-row blocks ran at ~3.2 TB/s on the level-0 shapes)
+// grid: (ceil(rows_per_stat / gs_rows), nstat); gs_rows (rows per block) is
+// sized on the host so the grid is one round of resident blocks (>= 64 rows each: the per-block fold
+// below is serial, so fewer, fuller blocks keep the pass streaming; 128-row blocks ran at ~3.2 TB/s)
 __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p, int gs_rows) {
   // per row lane, per channel partial sums (written once each, reduced in a fixed order below, so
   // the statistics are bit-reproducible): rows_par * 2C <= 8192 floats for C <= 4096
@@ -392,13 +392,30 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   if (nstat > 65535) return ACTH_EINVAL;
   if (hipMemsetAsync(d->ws, 0, (size_t)nstat * d->G * 2 * sizeof(double), stream) != hipSuccess)
     return ACTH_ELAUNCH;
-  int gs_rows = 512;
-  while (gs_rows > 128 && (long long)((d->rows_per_stat + gs_rows - 1) / gs_rows) * nstat < 1024) gs_rows >>= 1;
+  // Row span per statistics block: as many blocks as the chip holds at once (its 32 KB of LDS allow 5 per
+  // CU), split evenly over the statistics batches, so the pass is one full round of blocks (the former
+  // power-of-two spans gave 1512 blocks against 1280 slots at every UNet level: a second, 18 % round).
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gn_stats_kernel, 256, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 4;
+    slots = ncu * per_cu;
+  }
+  const long long per_stat = nstat >= slots ? 1 : slots / nstat;
+  int gs_rows = (int)((d->rows_per_stat + per_stat - 1) / per_stat);
+  if (gs_rows < 64) gs_rows = 64;
   dim3 g1((d->rows_per_stat + gs_rows - 1) / gs_rows, nstat);
   hipLaunchKernelGGL(gn_stats_kernel, g1, dim3(256), 0, stream, *d, gs_rows);
   ACTH_CHECK_LAUNCH();
   int rpb = 128;
   while (d->rows_per_stat % rpb) rpb >>= 1;
+  // fewer rows per block while the grid would not fill the chip twice over (2048 = 8 resident blocks on
+  // each of 256 CUs): the level-1 / level-2 shapes had 1512 / 378 blocks of 128 rows
+  while (rpb > 32 && (d->M / rpb) < 4096 && d->rows_per_stat % (rpb >> 1) == 0) rpb >>= 1;
   hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)(d->M / rpb)), dim3(256), 0, stream, *d, rpb);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;

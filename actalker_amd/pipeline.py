@@ -195,15 +195,24 @@ class HipBackend:
     def new_state(self, latents_all: torch.Tensor) -> torch.Tensor:
         return self.ops.nchw_to_tokens(latents_all.to(self.dev).float(), out_dtype=torch.float32)  # (T*S, 4)
 
+    def _dev_ints(self, values, dtype) -> torch.Tensor:
+        """Device copy of a small host index list, cached by content: the loop's index lists repeat every
+        step, and a host -> device copy from pageable memory blocks the host until the stream drains."""
+        cache = self.__dict__.setdefault("_ints", {})
+        key = (tuple(values), dtype)
+        t = cache.get(key)
+        if t is None:
+            t = cache[key] = torch.tensor(values, dtype=dtype).to(self.dev)
+        return t
+
     def run_units(self, lat: torch.Tensor, units: Sequence[Tuple[int, int]], frames: List[List[int]],
                   t: float, sigma: float, out: torch.Tensor, row0: int):
         """UNet on ``units``; noise rows written to out[row0 : row0 + U*F*S]."""
         ops, F, S = self.ops, self.F, self.S
         U = len(units)
-        fidx = torch.tensor([f for (w, _c) in units for f in frames[w]], dtype=torch.int32)
-        branch = torch.tensor([c for (_w, c) in units], dtype=torch.int64)
-        fidx_d = fidx.to(self.dev, non_blocking=True)
-        br_d = branch.to(self.dev, non_blocking=True)
+        fl_h = [f for (w, _c) in units for f in frames[w]]
+        fidx_d = self._dev_ints(fl_h, torch.int32)
+        br_d = self._dev_ints([c for (_w, c) in units], torch.int64)
         x = ops.window_input(lat, fidx_d, self.img, br_d.to(torch.int32), 1.0 / math.sqrt(sigma * sigma + 1.0),
                              U, F, S, self.T)
         fl = fidx_d.long()
@@ -211,10 +220,10 @@ class HipBackend:
         ehs = (self.ide[bl, fl], [self.aud[bl, fl], self.vas[bl, fl]])
         cak = {"ip_adapter_masks": self.masks, "acth_gate": self.gate}
         tt = torch.full((1,), t, device=self.dev, dtype=torch.float32)
-        prmap, pmax = fidx_d, int(fidx.max())
+        prmap, pmax = fidx_d, max(fl_h)
         if self.pose_P != self.T:
-            pr = torch.tensor([r % self.pose_P for (w, _c) in units for r in self._raw[w]], dtype=torch.int32)
-            prmap, pmax = pr.to(self.dev, non_blocking=True), int(pr.max())
+            pr = [r % self.pose_P for (w, _c) in units for r in self._raw[w]]
+            prmap, pmax = self._dev_ints(pr, torch.int32), max(pr)
         prefix_src = None
         if self.share_prefix:
             cls = self.prefix_classes()
@@ -231,8 +240,8 @@ class HipBackend:
         acc = torch.zeros_like(lat)
         cnt = torch.zeros(self.T, device=self.dev, dtype=torch.float32)
         for w, rows in enumerate(unit_rows):
-            offs = torch.tensor(rows, dtype=torch.int64).to(self.dev, non_blocking=True)
-            fidx = torch.tensor(frames[w], dtype=torch.int32).to(self.dev, non_blocking=True)
+            offs = self._dev_ints(rows, torch.int64)
+            fidx = self._dev_ints(frames[w], torch.int32)
             ops.cfg_euler_accum(gathered, offs, lat, fidx, guidance[0], guidance[1], guidance[2], sigma, sigma_next,
                                 acc, cnt, self.F, self.S)
         return ops.div_counter(acc, cnt, torch.empty_like(lat), self.T, self.S)

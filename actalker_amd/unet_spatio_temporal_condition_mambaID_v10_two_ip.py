@@ -306,6 +306,16 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         self._batched_ctx_projections(ctx)
         return ctx
 
+    def _dev_ints(self, values, device) -> torch.Tensor:
+        """int64 device copy of a small host list, cached by content (the sampler repeats the same
+        prefix maps every step; a pageable host -> device copy waits for the stream to drain)."""
+        cache = self.__dict__.setdefault("_acth_ints", {})
+        key = (tuple(values), str(device))
+        t = cache.get(key)
+        if t is None:
+            t = cache[key] = torch.tensor(values, dtype=torch.int64, device=device)
+        return t
+
     def _batched_ctx_projections(self, ctx):
         """The per-call inputs every ResBlock / cross attention projects on its own -- ``temb`` through
         each ResBlock's ``time_emb_proj`` (diffusers resnet.py: ~40 per call), the ID token through each
@@ -427,8 +437,8 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         if uniq is not None:
             Bu = len(uniq)
             pos = {b: i for i, b in enumerate(uniq)}
-            ui = torch.tensor(uniq, dtype=torch.int64, device=x_tok.device)
-            inv = torch.tensor([pos[prefix_src[b]] for b in range(B)], dtype=torch.int64, device=x_tok.device)
+            ui = self._dev_ints(uniq, x_tok.device)
+            inv = self._dev_ints([pos[prefix_src[b]] for b in range(B)], x_tok.device)
 
             def take(t, per):                # rows of the distinct elements (t holds B x per rows)
                 return t.reshape(B, per, *t.shape[1:]).index_select(0, ui).reshape(Bu * per, *t.shape[1:])

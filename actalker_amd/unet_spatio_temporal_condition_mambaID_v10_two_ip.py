@@ -375,13 +375,14 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         if ctx.has_ip:
             for key, attns, atok, vtok in (("s", sp, ctx.audio_tok, ctx.vasa_tok),
                                            ("t", tp, ctx.audio_mean, ctx.vasa_mean)):
-                procs = [(a, a.processor) for a in attns if modules.is_ip_processor(a.processor)]
-                if not procs:
-                    continue
-                for dst, zero, tok, srcs in (
-                        (ctx.ipkv, ctx.audio_zero, atok, [(pr.to_k_ip[0].weight, pr.to_v_ip[0].weight) for _, pr in procs]),
-                        (ctx.ipvb, ctx.vasa_zero, vtok, [(pr.to_v_ip[1].weight,) for _, pr in procs])):
-                    if zero or tok is None:
+                ip = [(a, a.processor) for a in attns if modules.is_ip_processor(a.processor)]
+                kv_procs = [(a, pr) for a, pr in ip if len(pr.to_k_ip) > 0 and len(pr.to_v_ip) > 0]
+                vb_procs = [(a, pr) for a, pr in ip if len(pr.to_v_ip) > 1]
+                for dst, zero, tok, procs, srcs in (
+                        (ctx.ipkv, ctx.audio_zero, atok, kv_procs,
+                         [(pr.to_k_ip[0].weight, pr.to_v_ip[0].weight) for _, pr in kv_procs]),
+                        (ctx.ipvb, ctx.vasa_zero, vtok, vb_procs, [(pr.to_v_ip[1].weight,) for _, pr in vb_procs])):
+                    if zero or tok is None or not procs:
                         continue
                     flat = [t for ws in srcs for t in ws]
                     w = modules._versioned_pack(self, ("ip", key, len(srcs[0])), flat,

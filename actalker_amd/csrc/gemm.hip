@@ -200,6 +200,7 @@ static int choose_tile(const ActhGemmDesc* d) {
   // 776916x104x640 311 -> 374 TF/s (256x128), 196308x144x1280 451 -> 516 and 51156x224x2560
   // 382 -> 773 (256x256 instead of 256x160), conv 774144x4x2880 17.7 -> 21.4.
   const bool tall = d->act != 2 && d->M >= 256 * 128;
+  if (tall && d->N <= 32) return 7;
   if (tall && d->N < 128) return 6;
   if (d->N < 128 || d->M < 256) return 1;
   const long long mt = (d->M + 255) / 256;
@@ -283,7 +284,7 @@ extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
   if (b_bytes >= 0x80000000LL) return ACTH_EINVAL;
   if (a_bytes >= 0x80000000LL || a2_bytes >= 0x80000000LL) return gemm_split_rows(d, stream);
   const int tile = choose_tile(d) & 0xff;
-  if (tile == 4 || tile == 5 || tile == 6)
+  if (tile >= 4 && tile <= 7)
     return gemm8p_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);
   if (tile == 2 || tile == 3)
     return gemm256_launch(d, tile, (unsigned)a_bytes, (unsigned)a2_bytes, (unsigned)b_bytes, vec_ok, stream);

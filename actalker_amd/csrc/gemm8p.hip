@@ -322,9 +322,12 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     if (more) stage_b(1, nxt);
     BAR();
     mma(acc[1][1]);
-    // A0(k+1), B0(k+1) are read in the next tile's phase 0 (B1(k+1)'s pieces may stay in flight)
-    if (NBP % 8 == 0 || nbw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    // A0(k+1), B0(k+1) are read in the next tile's phase 0: retire everything but this wave's B1(k+1)
+    // pieces (nbw: 3 / 2 for the 256x320 tile's two wave halves, 2 at 256x256, 1 at 256x128)
+    if (nbw >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (nbw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (nbw == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     BAR();
     // phase 3: quadrant (1,0); stage A1(k+1)
     read_b(cur, 0);
@@ -601,7 +604,8 @@ static int gemm8p_group_m(const ActhGemmDesc* d) {
 }
 
 // tile 4: 256 x 256; tile 5: 256 x 320; tile 6: 256 x 128 (the tall-skinny Mamba x_proj: N = 104 on
-// 776916 rows, HBM-bound on A). Tiles 5 / 6: no GEGLU (wave column shares are not granule pairs).
+// 776916 rows, HBM-bound on A); tile 7: 256 x 64 (the UNet conv_out, N = 4: a quarter of tile 6's
+// padded MFMA work). Tiles 5-7: no GEGLU (wave column shares are not granule pairs).
 int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                   int vec_ok, hipStream_t stream) {
   const int mt = (d->M + 255) / 256;
@@ -614,6 +618,8 @@ int gemm8p_launch(const ActhGemmDesc* d, int tile, unsigned a_bytes, unsigned a2
     launch8p<320>(&dd, dim3((d->N + 319) / 320, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
   } else if (tile == 6 && d->act != 2) {
     launch8p<128>(&dd, dim3((d->N + 127) / 128, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+  } else if (tile == 7 && d->act != 2) {
+    launch8p<64>(&dd, dim3((d->N + 63) / 64, mt), a_bytes, a2_bytes, b_bytes, vec_ok, stream);
   } else {
     return ACTH_EINVAL;
   }

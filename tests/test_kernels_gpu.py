@@ -227,10 +227,10 @@ def test_gemm_host_bounds_checks(dev):
         ops.gemm(a, w, out=torch.empty(300, 128, device=dev, dtype=torch.bfloat16), orow=(100, 110, 0))
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7])
 def test_gemm_tile_variants(dev, tile):
-    """Every tile kernel (128x128; 256x256 / 256x160 8-wave; phased 256x256 / 256x320 / 256x128) on all
-    A loaders, tails and epilogues."""
+    """Every tile kernel (128x128; 256x256 / 256x160 8-wave; phased 256x256 / 256x320 / 256x128 / 256x64)
+    on all A loaders, tails and epilogues."""
     from actalker_amd.modules import pack_conv3x3, pack_conv3d_t, pack_geglu
     # dense, ragged M/N/K + bias + residual + silu, fp32 out
     M, N, K = 700, 330, 200
@@ -281,7 +281,7 @@ def test_gemm_tile_variants(dev, tile):
     xg = bf(rnd(Mg, Cg))
     wg, bg = rnd(2 * inner, Cg, scale=Cg ** -0.5), rnd(2 * inner, scale=0.1)
     wp, bp = pack_geglu(wg, bg)
-    if tile in (3, 5, 6):
+    if tile in (3, 5, 6, 7):
         with pytest.raises(Exception):
             ops.gemm(xg.to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU, tile=tile)
     else:
@@ -298,6 +298,16 @@ def test_gemm_tall_skinny_auto_tile(dev):
     out = ops.gemm(a.to(dev), w.to(dev), out_f32=True)
     assert out.dtype == torch.float32
     assert rel(out, a.float() @ w.float().t()) < 1e-2
+    # conv_out class: 3x3 conv to 4 channels over >= 32768 output rows (256x64 tile), fp32 out + bias
+    from actalker_amd.modules import pack_conv3x3
+    B, H, W, C = 4, 72, 128, 320
+    x = bf(rnd(B, C, H, W))
+    wc = bf(rnd(4, C, 3, 3, scale=(9 * C) ** -0.5))
+    bias = rnd(4)
+    tok = x.permute(0, 2, 3, 1).reshape(-1, C).contiguous().to(dev)
+    out = ops.conv3x3(tok, pack_conv3x3(wc).to(dev), B, H, W, bias=bias.to(dev), out_f32=True)
+    refo = F.conv2d(x.float(), wc.float(), bias, padding=1).permute(0, 2, 3, 1).reshape(-1, 4)
+    assert rel(out, refo) < 1e-2
 
 
 @pytest.mark.parametrize("B,H,W,C1,C2,Cout,mode", [

@@ -1,4 +1,4 @@
-"""Micro-benchmark of GroupNorm (+SiLU) at the UNet's level shapes (random data), stats + apply passes.
+"""Micro-benchmark of GroupNorm (+SiLU, stats + apply passes) and LayerNorm at the UNet's level shapes.
 
   python tools/bench_norm.py        (ACTH_LIB=<other build> for an A/B of two libraries)
 """
@@ -32,6 +32,20 @@ def main(iters=20):
         us = 1000.0 * e0.elapsed_time(e1) / iters
         gbs = 2 * M * C * 2 / (us * 1e3)          # algorithmic: x read once, y written once
         print(f"groupnorm M={M} C={C} rows/stat={rps}: {us:.1f} us  {gbs:.0f} GB/s (algorithmic)", flush=True)
+
+    for M, C in ((774144, 320), (193536, 640), (48384, 1280)):
+        x = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
+        gamma, beta = torch.randn(C, generator=g).to(dev), torch.randn(C, generator=g).to(dev)
+        ops.layernorm(x, gamma, beta, 1e-5)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            ops.layernorm(x, gamma, beta, 1e-5)
+        e1.record()
+        torch.cuda.synchronize()
+        us = 1000.0 * e0.elapsed_time(e1) / iters
+        print(f"layernorm M={M} C={C}: {us:.1f} us  {2 * M * C * 2 / (us * 1e3):.0f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -165,6 +165,7 @@ SIGNATURES = {
     "acth_groupnorm_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
     "acth_mamba_combine_ln": ([_P(MambaCombineDesc), c_vp], c_int),
     "acth_selective_scan": ([_P(ScanDesc), c_vp], c_int),
+    "acth_selective_scan2": ([_P(ScanDesc), _P(ScanDesc), c_vp], c_int),
     "acth_selective_scan_workspace_size": ([c_int, c_int, c_int, c_int], ctypes.c_size_t),
     "acth_conv_direct": ([_P(ConvDirectDesc), c_vp], c_int),
     "acth_softmax_rows": ([c_vp, c_int, c_vp, c_int, c_int, c_int, c_float, c_vp], c_int),

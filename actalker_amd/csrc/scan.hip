@@ -238,8 +238,13 @@ __device__ __forceinline__ float pair_swap(float v) {
 // stages). The recurrence lanes then read delta with one ds_read: the per-token VALU dot product
 // (R/2 packed FMAs per lane), its pair reduction and the softplus that both lanes of a pair used to
 // repeat leave the serial loop.
+// Two descriptors: blocks with blockIdx.z < nb0 scan p0's batch elements, the rest p1's (the two SS2D
+// branches of one Mamba block in one launch, acth_selective_scan2); a single scan passes p1 = p0.
 template <int R, int CH, bool SOFTPLUS>
-__global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(const ActhScanDesc p) {
+__global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(const ActhScanDesc p0,
+                                                                             const ActhScanDesc p1, int nb0) {
+  const bool second = (int)blockIdx.z >= nb0;
+  const ActhScanDesc& p = *(second ? &p1 : &p0);  // wave-uniform: scalar loads from the kernarg segment
   constexpr int NT = 2 * CH;                     // threads
   constexpr int SP_CH = CH;
   constexpr int U16 = CH / 8;                    // 16-byte chunks per token row of the u / y tile
@@ -258,7 +263,7 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
   __shared__ __attribute__((aligned(16))) bf16_t ys[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) float dls[SC_T * DLP];
 
-  const int k = blockIdx.y, b = blockIdx.z;
+  const int k = blockIdx.y, b = (int)blockIdx.z - (second ? nb0 : 0);
   const int t = threadIdx.x;
   const int half = t & 1, cl = t >> 1;           // state half, channel within the block
   const int dbase = blockIdx.x * SP_CH;
@@ -507,8 +512,8 @@ static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
     // bench step (nb 84: 336 ten-wave blocks on 256 CUs run as two rounds; 840 four-wave blocks
     // balance), profiles/r2_step6_bench_scan_ch*.log, r2_step7_kernel_stats.csv.)
     const dim3 grid((d.D + 127) / 128, d.G, d.nb);
-    if (d.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true>), grid, dim3(256), 0, stream, d);
-    else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false>), grid, dim3(256), 0, stream, d);
+    if (d.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true>), grid, dim3(256), 0, stream, d, d, d.nb);
+    else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false>), grid, dim3(256), 0, stream, d, d, d.nb);
   } else {
     // pass 1: every chunk but the last records its end state
     hipLaunchKernelGGL((scan_kernel<R, 1>), dim3(gx, d.G, d.nb * (d.nchunks - 1)), dim3(SC_THREADS), 0, stream, d);
@@ -523,9 +528,8 @@ extern "C" size_t acth_selective_scan_workspace_size(int nb, int G, int D, int n
   return nchunks <= 1 ? 0 : (size_t)nb * G * nchunks * 17 * (size_t)D * sizeof(float);
 }
 
-extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
-  if (!dp) return ACTH_EINVAL;
-  ActhScanDesc d = *dp;
+// argument checks and derived fields (nchunks / chunk_len); 1 = valid with nothing to do (n_keep 0)
+static int scan_prepare(ActhScanDesc& d) {
   if (!d.u || !d.xdbl || !d.A_log || !d.y0) return ACTH_EINVAL;
   if (d.R > 0 && (!d.dt_w || d.delta)) return ACTH_EINVAL;          // exactly one delta source
   if (d.R == 0 && !d.delta) return ACTH_EINVAL;
@@ -533,7 +537,7 @@ extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
   if (d.G < 1 || d.G > 65535 || (d.flip1 && d.G != 2) || (d.y1 && d.G != 2)) return ACTH_EINVAL;
   if (d.n_keep < 0 || d.n_keep > d.L || d.ldx < d.G * (d.R + 32)) return ACTH_EINVAL;
   if (d.D % 8 || d.ldu % 8 || (d.delta && (d.D % 4 || d.ld_delta % 4))) return ACTH_EINVAL;
-  if (d.n_keep == 0) return ACTH_OK;
+  if (d.n_keep == 0) return 1;
   if (d.nchunks < 1) d.nchunks = 1;
   if (d.nchunks > d.L) d.nchunks = d.L;
   d.chunk_len = (d.L + d.nchunks - 1) / d.nchunks;
@@ -541,6 +545,17 @@ extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
   d.nchunks = (d.L + d.chunk_len - 1) / d.chunk_len;
   if (d.nchunks > 1 && !d.ws) return ACTH_EINVAL;
   if ((long long)d.nb * d.nchunks > 65535) return ACTH_EINVAL;
+  if (d.R != 0 && d.R != 1 && d.R != 2 && d.R != 3 && d.R != 4 && d.R != 5 && d.R != 6 && d.R != 8 &&
+      d.R != 16 && d.R != 20 && d.R != 40 && d.R != 80)
+    return ACTH_EINVAL;   // dt_rank = ceil(d_model / 16): 20/40/80 in the SVD UNet; 1,2,4 toy widths
+  return ACTH_OK;
+}
+
+extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
+  if (!dp) return ACTH_EINVAL;
+  ActhScanDesc d = *dp;
+  const int rc = scan_prepare(d);
+  if (rc != ACTH_OK) return rc == 1 ? ACTH_OK : rc;
   switch (d.R) {
     case 0: return launch_scan<0>(d, stream);
     case 1: return launch_scan<1>(d, stream);
@@ -554,6 +569,49 @@ extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
     case 20: return launch_scan<20>(d, stream);
     case 40: return launch_scan<40>(d, stream);
     case 80: return launch_scan<80>(d, stream);
-    default: return ACTH_EINVAL;   // dt_rank = ceil(d_model / 16): 20/40/80 in the SVD UNet; 1,2,4 toy widths
+    default: return ACTH_EINVAL;
+  }
+}
+
+template <int R>
+static int launch_scan2(const ActhScanDesc& a, const ActhScanDesc& b, hipStream_t stream) {
+  const dim3 grid((a.D + 127) / 128, a.G, a.nb + b.nb);
+  if (a.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true>), grid, dim3(256), 0, stream, a, b, a.nb);
+  else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false>), grid, dim3(256), 0, stream, a, b, a.nb);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
+// Two independent scans of the same kernel configuration (R, D, G, softplus, single pass) in one
+// launch: SS2D_cond_v10's audio and expression branches (mamba_layer.py:1955-1986, each an SS2D_Unit
+// scan, :1532-1538). One launch of both holds twice the waves, so the level-0 grid's last partial
+// round of waves (3360 waves on 1024 SIMDs per branch) is shared instead of paid twice.
+extern "C" int acth_selective_scan2(const ActhScanDesc* d0p, const ActhScanDesc* d1p, hipStream_t stream) {
+  if (!d0p || !d1p) return ACTH_EINVAL;
+  ActhScanDesc a = *d0p, b = *d1p;
+  const int ra = scan_prepare(a), rb = scan_prepare(b);
+  if ((ra != ACTH_OK && ra != 1) || (rb != ACTH_OK && rb != 1)) return ACTH_EINVAL;
+  if (ra == 1 || rb == 1 || a.nchunks > 1 || b.nchunks > 1 || a.R != b.R || a.D != b.D || a.G != b.G ||
+      a.softplus != b.softplus || (long long)a.nb + b.nb > 65535) {
+    // nothing to pair: the separate launches
+    int rc = ACTH_OK;
+    if (ra != 1) rc = acth_selective_scan(d0p, stream);
+    if (rc == ACTH_OK && rb != 1) rc = acth_selective_scan(d1p, stream);
+    return rc;
+  }
+  switch (a.R) {
+    case 0: return launch_scan2<0>(a, b, stream);
+    case 1: return launch_scan2<1>(a, b, stream);
+    case 2: return launch_scan2<2>(a, b, stream);
+    case 3: return launch_scan2<3>(a, b, stream);
+    case 4: return launch_scan2<4>(a, b, stream);
+    case 5: return launch_scan2<5>(a, b, stream);
+    case 6: return launch_scan2<6>(a, b, stream);
+    case 8: return launch_scan2<8>(a, b, stream);
+    case 16: return launch_scan2<16>(a, b, stream);
+    case 20: return launch_scan2<20>(a, b, stream);
+    case 40: return launch_scan2<40>(a, b, stream);
+    case 80: return launch_scan2<80>(a, b, stream);
+    default: return ACTH_EINVAL;
   }
 }

@@ -595,12 +595,16 @@ class SS2D_Unit(nn.Module):
     def _acth_invalidate(self):
         self.__dict__["_acth_cache"] = {}
 
-    def scan(self, u, nb, L, n_keep):
-        """u: (nb*L, d_inner) bf16 token-major sequence -> (y_dir0, y_dir1) for l < n_keep."""
+    def scan_args(self, u, nb, L, n_keep):
+        """x_proj of u (the GEMM ahead of the scan) and the scan's arguments."""
         p = self.packed()
         xdbl = ops.gemm(u, p["xproj"], out_f32=True)
-        return ops.selective_scan(u, xdbl, p["dt_w"], p["dt_b"], p["A_log"], p["D"], nb=nb, L=L,
-                                  R=self.dt_rank, n_keep=n_keep)
+        return dict(u=u, xdbl=xdbl, dt_w=p["dt_w"], dt_b=p["dt_b"], A_log=p["A_log"], Dskip=p["D"], nb=nb, L=L,
+                    R=self.dt_rank, n_keep=n_keep)
+
+    def scan(self, u, nb, L, n_keep):
+        """u: (nb*L, d_inner) bf16 token-major sequence -> (y_dir0, y_dir1) for l < n_keep."""
+        return ops.selective_scan(**self.scan_args(u, nb, L, n_keep))
 
 
 class SS2D_cond_v10(nn.Module):
@@ -629,8 +633,13 @@ class SS2D_cond_v10(nn.Module):
         self.out_proj = Linear(self.d_inner, d_model, bias=bias)
         self.scan_type = scan_type
 
-    def _branch(self, ctx: Ctx, h, S, info, in_proj: Linear, cond_proj: Linear, cond_tok, n_cond, unit):
-        """One masked branch: select tokens -> [tokens, ID, cond] -> bidirectional scan."""
+    # both branches' scans in one launch (acth_selective_scan2); False: one launch per branch
+    acth_pair_scan = True
+
+    def _branch(self, ctx: Ctx, h, S, info, in_proj: Linear, cond_proj: Linear, cond_tok, n_cond, unit,
+                defer=False):
+        """One masked branch: select tokens -> [tokens, ID, cond] -> bidirectional scan. defer: return the
+        scan's arguments under "scan" instead of running it (run() pairs the two branches)."""
         BF, Din = ctx.BF, self.d_inner
         n_sel = S if info is None else info.n_sel
         identity = info is None or info.identity
@@ -658,15 +667,25 @@ class SS2D_cond_v10(nn.Module):
             uv[:, n_sel + 1:n_sel + 1 + n_cond].copy_(cp.view(BF, n_cond, Din))
         else:
             ops.gemm(cond_tok, cond_proj.w(), act=ops.ACT_SILU, out=u, orow=(n_cond, L, n_sel + 1))
-        br["y0"], br["y1"] = unit.scan(u, BF, L, n_sel)
         br["L"] = n_sel          # scan outputs hold n_sel rows per batch element
+        if defer:
+            br["scan"] = unit.scan_args(u, BF, L, n_sel)
+        else:
+            br["y0"], br["y1"] = unit.scan(u, BF, L, n_sel)
         return br
 
     def run(self, ctx: Ctx, h, S):
         ia, ie = ctx.mask(0, S), ctx.mask(1, S)
+        pair = self.acth_pair_scan
         ba = self._branch(ctx, h, S, ia, self.in_proj1, self.audio_proj, ctx.audio_tok, ctx.n_audio,
-                          self.audio_unit)
-        be = self._branch(ctx, h, S, ie, self.in_proj2, self.exp_proj, ctx.vasa_tok, 1, self.exp_unit)
+                          self.audio_unit, defer=pair)
+        be = self._branch(ctx, h, S, ie, self.in_proj2, self.exp_proj, ctx.vasa_tok, 1, self.exp_unit,
+                          defer=pair)
+        if "scan" in ba and "scan" in be:
+            (ba["y0"], ba["y1"]), (be["y0"], be["y1"]) = ops.selective_scan2(ba.pop("scan"), be.pop("scan"))
+        for br in (ba, be):
+            if "scan" in br:
+                br["y0"], br["y1"] = ops.selective_scan(**br.pop("scan"))
         g, b = self.out_norm.gb()
         y = ops.mamba_combine_ln(ba, be, g, b, self.out_norm.eps, h.shape[0], S, self.d_inner)
         return ops.gemm(y, self.out_proj.w())

@@ -374,10 +374,8 @@ def mamba_combine_ln(branch_a: dict, branch_e: dict, gamma, beta, eps: float, M:
     return out
 
 
-def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip, *, nb: int, L: int, R: int,
-                   n_keep: int, y0=None, y1=None, nchunks: Optional[int] = None):
-    """Fused bidirectional scan. u: (nb*L, D) bf16, xdbl: (nb*L, 2*(R+32)) fp32."""
-    lib = _lib.load()
+def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks):
+    """Checks and ScanDesc of one fused bidirectional scan; (None, y0, y1, None) when n_keep is 0."""
     _need(u, torch.bfloat16, "scan u")
     _need(xdbl, torch.float32, "scan xdbl")
     D = u.shape[1]
@@ -390,7 +388,7 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
     if y1 is None:
         y1 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
     if n_keep == 0:
-        return y0, y1
+        return None, y0, y1, None
     d = _lib.ScanDesc()
     d.u, d.ldu = u.data_ptr(), _rows(u, "scan u")
     d.xdbl, d.ldx = xdbl.data_ptr(), _rows(xdbl, "scan xdbl")
@@ -399,9 +397,36 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
     d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, R, 16, n_keep
     d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = 1, 2, 0, 0, 1
     ws = _scan_chunking(d, nb, 2, D, L, nchunks, u.device)
-    _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
+    return d, y0, y1, ws
+
+
+def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip, *, nb: int, L: int, R: int,
+                   n_keep: int, y0=None, y1=None, nchunks: Optional[int] = None):
+    """Fused bidirectional scan. u: (nb*L, D) bf16, xdbl: (nb*L, 2*(R+32)) fp32."""
+    lib = _lib.load()
+    d, y0, y1, ws = _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks)
+    if d is not None:
+        _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
     del ws
     return y0, y1
+
+
+def selective_scan2(a: dict, b: dict):
+    """Two fused bidirectional scans (selective_scan's keyword arguments each: u, xdbl, dt_w, dt_b,
+    A_log, Dskip, nb, L, R, n_keep) in one launch -- SS2D_cond_v10's audio and expression branches.
+    Returns ((y0, y1) of a, (y0, y1) of b)."""
+    lib = _lib.load()
+    da, ya0, ya1, wsa = _fused_scan_desc(nchunks=1, y0=None, y1=None, **a)
+    db, yb0, yb1, wsb = _fused_scan_desc(nchunks=1, y0=None, y1=None, **b)
+    if da is not None and db is not None:
+        _lib.check(lib.acth_selective_scan2(ctypes.byref(da), ctypes.byref(db), _stream()),
+                   "acth_selective_scan2")
+    else:
+        for d in (da, db):
+            if d is not None:
+                _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
+    del wsa, wsb
+    return (ya0, ya1), (yb0, yb1)
 
 
 def scan_auto_chunks(nb: int, G: int, D: int, L: int) -> int:

@@ -346,6 +346,8 @@ def main():
                          "between the branches whose prefix inputs are equal)")
     ap.add_argument("--no-batch-ctx-proj", action="store_true",
                     help="per-module time_emb_proj / to_v(ID) GEMMs instead of the three batched ones per UNet call")
+    ap.add_argument("--no-pair-scan", action="store_true",
+                    help="one scan launch per Mamba branch instead of one launch for both branches")
     ap.add_argument("--no-dedup", action="store_true",
                     help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
     ap.add_argument("--no-four-branch-compare", action="store_true",
@@ -379,6 +381,11 @@ def main():
     unet_cpu = build_unet(dev)
     unet = unet_cpu.to(dev)
     unet.acth_batch_ctx_projections = not args.no_batch_ctx_proj
+    if args.no_pair_scan:
+        from actalker_amd import modules as _m
+        for mod in unet.modules():
+            if isinstance(mod, _m.SS2D_cond_v10):
+                mod.acth_pair_scan = False
     log(f"model built in {time.time() - t0:.1f}s")
     inp = synthetic_inputs(N, fpb, H, W, args.mode)
     backend = pl.HipBackend(unet, H // 8, W // 8, inp["masks"], gate, inp["added"], N + fpb, fpb,

@@ -166,6 +166,10 @@ typedef struct ActhScanDesc {
   float* ws;                  /* acth_selective_scan_workspace_size(nb, G, D, nchunks) bytes */
 } ActhScanDesc;
 int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream);
+/* Both SS2D branches of SS2D_cond_v10 (audio d0, expression d1; mamba_layer.py:1955-1986) in one
+ * launch when they share R, D, G, softplus and are single-pass; otherwise two launches. Each
+ * descriptor means exactly what it means to acth_selective_scan. */
+int acth_selective_scan2(const ActhScanDesc* d0, const ActhScanDesc* d1, hipStream_t stream);
 size_t acth_selective_scan_workspace_size(int nb, int G, int D, int nchunks);
 
 /* ---- direct 3x3 (pad 1, stride 1/2) / temporal (3,1,1) convolution for narrow channel counts

@@ -559,6 +559,27 @@ def test_selective_scan_fused(dev, nb, L, D, R, n_keep, nchunks):
     assert rel(y1, r1) < 1e-2
 
 
+@pytest.mark.parametrize("ca,cb", [
+    ((2, 300, 640, 20, 267), (2, 45, 640, 20, 40)),        # same kernel config, different L / n_keep
+    ((3, 97, 1280, 40, 64), (1, 33, 1280, 40, 33)),        # different nb
+    ((2, 40, 64, 4, 30), (2, 40, 64, 8, 30)),              # different R: two launches
+    ((2, 40, 64, 4, 0), (2, 50, 64, 4, 50))])              # one branch empty
+def test_selective_scan2_matches_single(dev, ca, cb):
+    """acth_selective_scan2 (both SS2D branches in one launch) == two acth_selective_scan calls, bit for bit."""
+    args, singles = [], []
+    for i, (nb, L, D, R, n_keep) in enumerate((ca, cb)):
+        g = torch.Generator().manual_seed(7 + i * 31 + L)
+        u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
+        xdbl = u.float() @ bf(xproj).float().t()
+        a = dict(u=u.to(dev), xdbl=xdbl.to(dev), dt_w=dtw.to(dev), dt_b=dtb.to(dev), A_log=alog.to(dev),
+                 Dskip=Dp.to(dev), nb=nb, L=L, R=R, n_keep=n_keep)
+        args.append(a)
+        singles.append(ops.selective_scan(**a))
+    pair = ops.selective_scan2(args[0], args[1])
+    for (p0, p1), (s0, s1) in zip(pair, singles):
+        assert torch.equal(p0, s0) and torch.equal(p1, s1)
+
+
 def test_selective_scan_fn_dropin(dev):
     """actalker_amd.selective_scan_interface.selective_scan_fn == mamba-ssm semantics (op mode)."""
     from actalker_amd.selective_scan_interface import selective_scan_fn

@@ -192,6 +192,32 @@ def test_batched_ctx_projections_match_per_module(dev, tiny):
     assert rel(batched, single) < 1e-3
 
 
+def test_paired_mamba_scan_matches_per_branch(dev, tiny):
+    """SS2D_cond_v10 with both branches' scans in one acth_selective_scan2 launch == one launch per branch,
+    bit for bit (the tiny inputs' masks select part of each frame, so both branches scan)."""
+    from actalker_amd import modules, ops
+    unet, sd, cfg = tiny
+    sample, t, ehs, added, pose, masks = ge._tiny_inputs(B=3, F=3, H=16, W=32, seed=11)
+    B, F, H, W = 3, 3, 16, 32
+    x = ops.nchw_to_tokens(sample.to(dev))
+    sc = ops.nchw_to_tokens(pose.to(dev))
+    e = (ehs[0].to(dev), [a.to(dev) for a in ehs[1]])
+    cak = {"ip_adapter_masks": masks}
+    mods = [m for m in unet.modules() if isinstance(m, modules.SS2D_cond_v10)]
+    assert mods
+    try:
+        with torch.no_grad():
+            paired = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak)
+            for m in mods:
+                m.acth_pair_scan = False
+            single = unet.forward_tokens(x, B, F, H, W, t.to(dev), e, added.to(dev), sc, cak)
+    finally:
+        for m in mods:
+            m.acth_pair_scan = True
+    assert torch.isfinite(paired.float()).all()
+    assert torch.equal(paired, single)
+
+
 def test_pipeline_prefix_sharing_matches_unshared_loop(dev, tiny):
     """The sampler loop with LoopConfig.share_cfg_prefix on and off, CFG inputs shaped as the reference
     builds them (pipeline:162-205: branch 0 zero image latents / ID, branches 1-3 equal image latents;

@@ -1,0 +1,97 @@
+"""Cases of the REFERENCE-RUN UNet forward goldens, shared by
+tools/gen_golden_unet_ref.py (runs the reference's own UNet package on the CPU) and the tests.
+
+The fixtures pin the reference's orchestration -- unet_spatio_temporal_condition_mambaID_v10_two_ip.py
+:362-517, unet_3d_blocks.py:2047-2592, TransformerSTmodel.py:4001-4155 (and the plain mid transformer
+:200-421), attention.py:223-343 / 418-473, attention_processor.py:1528-1605 / 2747-2934, mamba_layer.py
+:1394-1553 / 1902-1986 -- executed unchanged; only the diffusers 0.29.2 leaves (oracle/diffusers_leaves.py)
+and mamba-ssm's selective_scan_ref are restatements.
+
+* ``tiny_*``: the full UNet topology (4 down / mid / 4 up blocks, 15 v10 transformers with Mamba, IP
+  adapters) at widths 64/128/128/128, heads 1/2/2/2, B = 2 CFG branches x F = 3 frames, latent 16x32
+  (128x256 px masks). Mask cases follow the pipeline's gates (pipeline:702-711): mode0 [face, 0] with
+  zero VASA tokens, mode1 [0, face] with zero audio tokens, mode2 [ones, ones], half [mouth (lower
+  half), expression (upper half)], box [centre box, upper half] (a partial mask whose token rows are
+  not whole image rows).
+* ``full_half``: the real 1.775 B-parameter UNet (widths 320/640/1280/1280, heads 5/10/20/20) at
+  576x1024, B = 1 x F = 2, half masks: the inputs and weights of tests/golden_full.py's ``half`` case,
+  so the same fixture also pins the oracle's full-geometry output.
+
+Weights are actalker_amd.synthetic values by parameter name (reference names: the key sets are equal,
+tests/test_checkpoint_cpu.py), regenerated from the seed on every host; the fixtures hold outputs and
+checksums only.
+"""
+import math
+
+import torch
+
+TINY_CFG = dict(block_out_channels=(64, 128, 128, 128), num_attention_heads=(1, 2, 2, 2), cross_attention_dim=1024,
+                layers_per_block=2, num_frames=3)
+TINY_SEED = 5
+TINY_B, TINY_F, TINY_H, TINY_W = 2, 3, 16, 32
+TINY_CASES = ("tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box")
+FULL_CASES = ("full_half",)
+CASES = TINY_CASES + FULL_CASES
+SIGMA = 1.6555  # Karras step 12 of 25; t = 0.25 ln sigma
+
+
+def tiny_inputs(case: str, seed: int = 23):
+    g = torch.Generator().manual_seed(seed)
+    B, F, h, w = TINY_B, TINY_F, TINY_H, TINY_W
+    sample = torch.randn(B, F, 8, h, w, generator=g)
+    t = torch.tensor(0.25 * math.log(SIGMA))
+    ide = torch.randn(B * F, 1, 1024, generator=g)
+    aud = torch.randn(B * F, 32, 1024, generator=g)
+    vas = torch.randn(B * F, 1, 1024, generator=g)
+    pose = 0.1 * torch.randn(B, F, TINY_CFG["block_out_channels"][0], h, w, generator=g)
+    added = torch.tensor([[12.5, 12.0, 20.0]] * B)
+    Hp, Wp = 8 * h, 8 * w
+    one, zero = torch.ones(1, 1, Hp, Wp), torch.zeros(1, 1, Hp, Wp)
+    face = zero.clone()
+    face[..., Hp // 4: 3 * Hp // 4, 5 * Wp // 16: 11 * Wp // 16] = 1.0
+    lower = zero.clone()
+    lower[..., Hp // 2:, :] = 1.0
+    kind = case.split("_", 1)[1]
+    if kind == "mode0":
+        masks, vas = [face, zero], torch.zeros_like(vas)
+    elif kind == "mode1":
+        masks, aud = [zero, face], torch.zeros_like(aud)
+    elif kind == "mode2":
+        masks = [one, one]
+    elif kind == "half":
+        masks = [lower, 1.0 - lower]
+    elif kind == "box":
+        masks = [face, 1.0 - lower]
+    else:
+        raise ValueError(case)
+    return sample, t, (ide, [aud, vas]), added, pose, masks
+
+
+def case_inputs(case: str):
+    if case in TINY_CASES:
+        return tiny_inputs(case)
+    if case == "full_half":
+        from tests import golden_full as gf
+        return gf.case_inputs("half")
+    raise ValueError(case)
+
+
+def build_hip_unet(case: str):
+    """The product UNet with the case's synthetic weights (CPU; caller moves it)."""
+    if case in FULL_CASES:
+        from tests import golden_full as gf
+        return gf.build_full_unet()
+    from actalker_amd.synthetic import init_synthetic_
+    from actalker_amd.unet_spatio_temporal_condition_mambaID_v10_two_ip import (UNetSpatioTemporalConditionModel,
+                                                                               add_ip_adapters)
+    torch.manual_seed(0)
+    unet = UNetSpatioTemporalConditionModel(**TINY_CFG)
+    add_ip_adapters(unet, [32, 32], [1.25, 1.25])
+    init_synthetic_(unet, TINY_SEED)
+    return unet
+
+
+def oracle_cfg(case: str):
+    if case in FULL_CASES:
+        return None
+    return dict(block_out_channels=TINY_CFG["block_out_channels"], num_attention_heads=TINY_CFG["num_attention_heads"])

@@ -20,6 +20,23 @@ CASES = {
     "c320_mode2": dict(seed=21, d_model=320, d_cond=1024, BF=2, S=144, mask_hw=(72, 128), masks="ones_ones"),
     "c320_mode1": dict(seed=22, d_model=320, d_cond=1024, BF=2, S=144, mask_hw=(72, 128), masks="zeros_ones"),
     "c320_half": dict(seed=23, d_model=320, d_cond=1024, BF=2, S=144, mask_hw=(72, 128), masks="lower_upper"),
+    "c320_mode0": dict(seed=24, d_model=320, d_cond=1024, BF=2, S=144, mask_hw=(72, 128), masks="ones_zeros"),
+}
+
+# Level shapes of the BASELINE geometry: the real 576x1024 masks downsampled to the
+# level's token grid (72x128 / 36x64 / 18x32, mamba_layer.py:1962-1981) and the real sequence lengths
+# (L = S + 33 audio / S + 2 expression). Inputs are regenerated from the seed; the fixtures
+# (tests/golden/ss2d_level_<case>.safetensors) hold the reference output at every ``sub``-th token row,
+# the input checksum and the selected-token counts.
+LEVEL_CASES = {
+    "l0_mode2": dict(seed=31, d_model=320, d_cond=1024, BF=1, S=9216, mask_hw=(576, 1024), masks="ones_ones", sub=7),
+    "l0_mode0": dict(seed=32, d_model=320, d_cond=1024, BF=1, S=9216, mask_hw=(576, 1024), masks="ones_zeros", sub=7),
+    "l0_box": dict(seed=33, d_model=320, d_cond=1024, BF=2, S=9216, mask_hw=(576, 1024), masks="box_upper", sub=7),
+    "l1_half": dict(seed=34, d_model=640, d_cond=1024, BF=2, S=2304, mask_hw=(576, 1024), masks="lower_upper", sub=3),
+    "l1_box": dict(seed=35, d_model=640, d_cond=1024, BF=1, S=2304, mask_hw=(576, 1024), masks="lower_box", sub=3),
+    "l2_mode2": dict(seed=36, d_model=1280, d_cond=1024, BF=2, S=576, mask_hw=(576, 1024), masks="ones_ones", sub=1),
+    "l2_mode1": dict(seed=37, d_model=1280, d_cond=1024, BF=2, S=576, mask_hw=(576, 1024), masks="zeros_ones", sub=1),
+    "l2_box": dict(seed=38, d_model=1280, d_cond=1024, BF=1, S=576, mask_hw=(576, 1024), masks="box_lower", sub=1),
 }
 
 
@@ -59,6 +76,8 @@ def _mask(kind: str, hw):
         m[..., H // 2:, :] = 1.0
     elif kind == "upper":
         m[..., : H // 2, :] = 1.0
+    elif kind == "box":                      # a face box whose edges fall between latent rows / columns
+        m[..., int(0.26 * H): int(0.74 * H), int(0.33 * W): int(0.69 * W)] = 1.0
     return m
 
 

@@ -639,3 +639,28 @@ def test_cfg_euler_accum(dev):
     got = acc.cpu().view(T, S, 4)
     torch.testing.assert_close(got[fidx.long()], xn, rtol=1e-5, atol=1e-5)
     assert cnt.cpu().tolist() == [1, 0, 0, 0, 1, 1]
+
+
+def test_cfg_euler_accum_matches_reference_scheduler_mirror(dev):
+    """acth_cfg_euler_accum's Euler part at all 25 Karras steps against the REFERENCE scheduler mirror's
+    ``step`` (scheduling_euler_discrete.py:80-207, tests/golden/euler_mirror.safetensors): with
+    g1 = g2 = g3 = 0 the guided prediction is the uncond branch, so the kernel's output is exactly one
+    v-prediction Euler step of it. fp32 state: rtol 1e-5."""
+    import os
+    from safetensors.torch import load_file
+    g = load_file(os.path.join(os.path.dirname(__file__), "golden", "euler_mirror.safetensors"))
+    _, F_, C, h, w = g["sample"].shape[1:]
+    S = h * w
+    sig = g["sigmas"].tolist()
+    rows = lambda t: t.reshape(F_, C, S).permute(0, 2, 1).reshape(F_ * S, C).contiguous()   # noqa: E731
+    for i in range(25):
+        mo = rows(g["model_out"][i])
+        noise = torch.cat([mo, torch.zeros(3 * F_ * S, C)]).to(dev)
+        offs = torch.tensor([0, F_ * S, 2 * F_ * S, 3 * F_ * S], dtype=torch.int64, device=dev)
+        lat = rows(g["sample"][i]).to(dev)
+        fidx = torch.arange(F_, dtype=torch.int32, device=dev)
+        acc = torch.zeros(F_ * S, C, device=dev)
+        cnt = torch.zeros(F_, device=dev)
+        ops.cfg_euler_accum(noise, offs, lat, fidx, 0.0, 0.0, 0.0, sig[i], sig[i + 1], acc, cnt, F_, S)
+        want = rows(g["prev"][i])
+        torch.testing.assert_close(acc.cpu(), want, rtol=1e-5, atol=1e-5 * (1 + sig[i]))

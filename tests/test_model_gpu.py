@@ -47,6 +47,35 @@ def test_ss2d_cond_v10_matches_reference_golden(dev, name):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("name", ["l0_mode2", "l0_mode0", "l0_box", "l1_half", "l1_box", "l2_mode2", "l2_mode1",
+                                  "l2_box"])
+def test_ss2d_cond_v10_level_shapes_match_reference(dev, name):
+    """SS2D_cond_v10 at the BASELINE level shapes -- S = 9216 / 2304 / 576 (scans of L = S + 33 / S + 2), the
+    real 576x1024 masks truncated to the level grids (mamba_layer.py:1962-1981) -- against the reference
+    module's own outputs (tools/gen_golden.py levels), every ``sub``-th token row. Tolerance rel-L2 <= 2e-2."""
+    from actalker_amd.modules import Ctx, SS2D_cond_v10
+    from tests import golden_full as gf
+    from tests.golden_weights import LEVEL_CASES
+    case = LEVEL_CASES[name]
+    g = load_file(os.path.join(GOLD, f"ss2d_level_{name}.safetensors"))
+    x, id_emb, conds, masks = make_inputs(case)
+    torch.testing.assert_close(gf.checksum(x, id_emb, conds, *masks), g["inputs_checksum"], rtol=1e-6, atol=1e-6)
+    m = SS2D_cond_v10(d_model=case["d_model"], d_cond=case["d_cond"], cond_size=32, dropout=0.1, d_state=16,
+                      size=8, scan_type="sweep", num_direction=2)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict(golden_weights(case["seed"], shapes), strict=True)
+    m = m.to(dev)
+    BF, S, C = x.shape
+    ctx = Ctx(BF, 1, dev)
+    ctx.id_tok = id_emb.reshape(BF, -1).to(dev, torch.bfloat16)
+    ctx.audio_tok = conds[:, :32].reshape(BF * 32, -1).to(dev, torch.bfloat16)
+    ctx.vasa_tok = conds[:, 32].reshape(BF, -1).to(dev, torch.bfloat16)
+    ctx.masks = masks
+    y = m.run(ctx, x.reshape(BF * S, C).to(dev, torch.bfloat16), S)
+    err = rel(y.view(BF, S, C)[:, ::case["sub"]], g["y_sub"])
+    assert err < 2e-2, err
+
+
 def _oracle_cfg(cfg):
     return dict(block_out_channels=cfg["block_out_channels"], num_attention_heads=cfg["num_attention_heads"])
 

@@ -133,3 +133,72 @@ def test_oracle_attention_matches_reference_processor_golden(name):
     want = load_file(os.path.join(GOLD, f"attn_{name}.safetensors"))["y"]
     got = ga.subsample(y, case)
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
+
+
+# ------------------------------------------------------------------------------------------
+# the oracle's whole UNet forward against the REFERENCE UNet package run on the CPU
+# (tools/gen_golden_unet_ref.py: v10 UNet / unet_3d_blocks / TransformerSTmodel / attention /
+# attention_processor / mamba_layer executed unchanged, diffusers leaves = oracle/diffusers_leaves.py)
+@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box"])
+def test_oracle_unet_matches_reference_run(case):
+    from tests import golden_full as gf
+    from tests import golden_unet_ref as gu
+    g = load_file(os.path.join(GOLD, f"unet_ref_{case}.safetensors"))
+    unet = gu.build_hip_unet(case)          # weights only: synthetic values by reference parameter name
+    sd = {k: v.detach().float() for k, v in unet.state_dict().items()}
+    torch.testing.assert_close(gf.checksum(*[sd[k] for k in sorted(sd)]), g["weights_checksum"], rtol=1e-9, atol=1e-6)
+    sample, t, ehs, added, pose, masks = gu.case_inputs(case)
+    torch.testing.assert_close(gf.checksum(sample, ehs[0], *ehs[1], pose, *masks), g["inputs_checksum"],
+                               rtol=1e-9, atol=1e-6)
+    with torch.no_grad():
+        out = ref.unet_forward(sd, sample, t, ehs, added, pose, {"ip_adapter_masks": masks}, cfg=gu.oracle_cfg(case))
+    rel = ((out - g["out"]).norm() / g["out"].norm()).item()
+    assert rel < 1e-4, rel
+
+
+def test_oracle_full_geometry_fixture_matches_reference_run():
+    """The full-geometry oracle fixture (576x1024, real widths, half masks; tools/gen_golden_full.py) against
+    the reference UNet run on the same weights and inputs (both checksums equal)."""
+    o = load_file(os.path.join(GOLD, "unet_full_half.safetensors"))
+    r = load_file(os.path.join(GOLD, "unet_ref_full_half.safetensors"))
+    torch.testing.assert_close(o["weights_checksum"], r["weights_checksum"], rtol=1e-9, atol=1e-6)
+    torch.testing.assert_close(o["inputs_checksum"], r["inputs_checksum"], rtol=1e-9, atol=1e-6)
+    rel = ((o["out"] - r["out"]).norm() / r["out"].norm()).item()
+    assert rel < 1e-4, rel
+
+
+# ------------------------------------------------------------------------------------------
+# SS2D_cond_v10 at the BASELINE level shapes (576x1024 masks, S = 9216 / 2304 / 576): reference module outputs
+@pytest.mark.parametrize("name", ["l0_mode2", "l0_mode0", "l0_box", "l1_half", "l1_box", "l2_mode2", "l2_mode1",
+                                  "l2_box"])
+def test_oracle_ss2d_level_shapes_match_reference(name):
+    from tests import golden_full as gf
+    from tests.golden_weights import LEVEL_CASES
+    from actalker_amd.masks import mask_info
+    case = LEVEL_CASES[name]
+    g = load_file(os.path.join(GOLD, f"ss2d_level_{name}.safetensors"))
+    x, id_emb, conds, masks = make_inputs(case)
+    torch.testing.assert_close(gf.checksum(x, id_emb, conds, *masks), g["inputs_checksum"], rtol=1e-9, atol=1e-6)
+    # the product's host-side token selection (masks.py) selects what the reference's int() truncation does
+    assert [mask_info(m, case["S"], "cpu").n_sel for m in masks] == g["n_selected"].tolist()
+    sd = golden_weights(case["seed"], _ss2d_shapes(case["d_model"], case["d_cond"]))
+    y = ref.ss2d_cond_v10({("m." + k): v for k, v in sd.items()}, "m", x, id_emb, conds, masks)
+    torch.testing.assert_close(y[:, ::case["sub"]], g["y_sub"], rtol=5e-5, atol=5e-5)
+
+
+# ------------------------------------------------------------------------------------------
+# Euler v-prediction step / add_noise against the REFERENCE scheduler mirror
+# (src/schedulers/scheduling_euler_discrete.py:47-207 run by tools/gen_golden_euler.py)
+def test_oracle_euler_step_matches_reference_mirror():
+    from actalker_amd import pipeline as pl
+    g = load_file(os.path.join(GOLD, "euler_mirror.safetensors"))
+    sig, ts = ref.euler_karras_tables(25)
+    torch.testing.assert_close(sig, g["sigmas"], rtol=0, atol=0)
+    torch.testing.assert_close(ts, g["timesteps"], rtol=0, atol=0)
+    psig, pts = pl.karras_sigmas(25)                       # the product's host-side tables
+    assert psig == g["sigmas"].tolist() and pts == g["timesteps"].tolist()
+    for i in range(25):
+        got = ref.euler_step_v(g["model_out"][i], sig[i], sig[i + 1], g["sample"][i])
+        torch.testing.assert_close(got, g["prev"][i], rtol=1e-5, atol=1e-5 * (1 + float(sig[i])))
+    # add_noise at the first timestep (pipeline:312-314): x0 + eps * sigma_0
+    torch.testing.assert_close(g["ref_latents"] + g["noise"] * sig[0], g["noised"], rtol=1e-6, atol=1e-4)

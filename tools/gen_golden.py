@@ -12,7 +12,8 @@ Weights are a deterministic function of a seed (``golden_weights``), so tests re
 instead of storing them. Fixtures written: tests/golden/ss2d_cond_v10_<case>.safetensors holding
 inputs (x, id_emb, conds, masks) and the reference output ``y``; plus a JSON index.
 
-Usage:  python tools/gen_golden.py
+Usage:  python tools/gen_golden.py            (toy / c320 cases, full tensors)
+        python tools/gen_golden.py levels [case ...]   (LEVEL_CASES: 576x1024 masks, real S; ~1-2 min)
 """
 from __future__ import annotations
 
@@ -20,6 +21,7 @@ import importlib.util
 import json
 import os
 import sys
+import time
 import types
 
 import torch
@@ -28,7 +30,8 @@ from safetensors.torch import save_file
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle.reference_cpu import mask_downsample, selective_scan_ref  # noqa: E402
-from tests.golden_weights import golden_weights, CASES, make_inputs  # noqa: E402
+from tests.golden_weights import golden_weights, CASES, LEVEL_CASES, make_inputs  # noqa: E402
+from tests.golden_full import checksum  # noqa: E402
 
 REF = "/root/reference/src/models/base/mamba_layer.py"
 OUT = os.path.join(ROOT, "tests", "golden")
@@ -72,9 +75,33 @@ def load_reference_mamba():
     return mod
 
 
+def level_main(ref, names):
+    """Level-shape cases: reference output at every ``sub``-th token row plus checksums (inputs regenerate)."""
+    for name in names:
+        case = LEVEL_CASES[name]
+        m = ref.SS2D_cond_v10(d_model=case["d_model"], d_cond=case["d_cond"], cond_size=32, dropout=0.1,
+                              d_state=16, size=8, scan_type="sweep", num_direction=2)
+        sd = golden_weights(case["seed"], {k: tuple(v.shape) for k, v in m.state_dict().items()})
+        m.load_state_dict(sd, strict=True)
+        m.eval()
+        x, id_emb, conds, masks = make_inputs(case)
+        n_sel = [int(mask_downsample(mk[:, 0], 1, case["S"], 1).view(-1).int().nonzero().numel()) for mk in masks]
+        t0 = time.time()
+        with torch.no_grad():
+            y = m(x, id_emb, conds, masks)
+        ysub = y[:, ::case["sub"]].contiguous()
+        save_file({"y_sub": ysub, "inputs_checksum": checksum(x, id_emb, conds, *masks),
+                   "n_selected": torch.tensor(n_sel, dtype=torch.int64)},
+                  os.path.join(OUT, f"ss2d_level_{name}.safetensors"))
+        print(name, tuple(y.shape), "selected", n_sel, f"{time.time() - t0:.1f}s", float(y.abs().mean()), flush=True)
+
+
 def main():
     ref = load_reference_mamba()
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "levels":
+        level_main(ref, sys.argv[2:] or list(LEVEL_CASES))
+        return
     index = {}
     for name, case in CASES.items():
         m = ref.SS2D_cond_v10(d_model=case["d_model"], d_cond=case["d_cond"], cond_size=32, dropout=0.1,

@@ -216,21 +216,32 @@ static int choose_tile(const ActhGemmDesc* d) {
 // consecutive launches over row chunks whose A extents fit, the descriptor rebased per chunk: rows
 // of C / R / MIX and row-bias images shifted, A (and A2) advanced by the chunk's first source row.
 // A chunk is whole units of the A mode -- any rows (dense), whole images (conv: the 3x3 taps stay
-// inside an image), whole batch elements (temporal: the frame taps stay inside one) -- and whole
-// row-bias images. Row remaps (rmap, orow) are not rebased: such calls keep the 2 GiB limit.
-// (The 112-frame mode-2 UNet call at 576x1024 reads 2.7 GB Mamba xz rows through x_proj.)
+// inside an image), whole batch elements (temporal: the frame taps stay inside one) -- whole
+// row-bias images and whole output-row-remap groups (orow_div source rows land orow_stride output
+// rows apart: a chunk starting at source row m0 = j * orow_div starts its C at output row
+// j * orow_stride, orow_off kept). Residual row maps (rmap) are not rebased: such calls keep the
+// 2 GiB limit. (The 112-frame mode-2 UNet call at 576x1024 reads 2.7 GB Mamba xz rows through x_proj;
+// with every token selected, the in_proj GEMM writes its level-0 xz rows through an orow remap.)
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream);
 
+static long long lcm_ll(long long a, long long b) {
+  long long g = a, r = b;
+  while (r) { const long long t = g % r; g = r; r = t; }
+  return a / g * b;
+}
+
 static int gemm_split_rows(const ActhGemmDesc* d, hipStream_t stream) {
-  if (d->rmap || d->orow_div < d->M) return ACTH_EINVAL;
+  if (d->rmap) return ACTH_EINVAL;
+  const bool remap = d->orow_div < d->M;
   long long unit_rows = 1, unit_arows = 1;                 // output rows / A rows per indivisible unit
   if (d->amode == 1) { unit_rows = (long long)d->Ho * d->Wo; unit_arows = (long long)d->H * d->W; }
   if (d->amode == 2) { unit_rows = unit_arows = (long long)d->F * d->S; }
-  if (d->rowbias) {
-    long long g = unit_rows, r = d->rb_div;                // unit := lcm(unit, rb_div) output rows
-    while (r) { const long long t = g % r; g = r; r = t; }
-    const long long mult = d->rb_div / g;
-    unit_rows *= mult; unit_arows *= mult;
+  long long need = 1;                                      // output-row multiples a chunk must keep
+  if (d->rowbias) need = lcm_ll(need, d->rb_div);
+  if (remap) need = lcm_ll(need, d->orow_div);
+  {
+    const long long lu = lcm_ll(unit_rows, need), mult = lu / unit_rows;
+    unit_rows = lu; unit_arows *= mult;
   }
   if (d->M % unit_rows && d->amode != 0) return ACTH_EINVAL;
   const long long lda_max = d->A2 ? (d->lda > d->lda2 ? d->lda : d->lda2) : d->lda;
@@ -244,11 +255,12 @@ static int gemm_split_rows(const ActhGemmDesc* d, hipStream_t stream) {
     c.M = (int)mc;
     c.A = (const char*)d->A + a0 * d->lda * 2;
     if (d->A2) c.A2 = (const char*)d->A2 + a0 * d->lda2 * 2;
-    c.C = (char*)d->C + m0 * d->ldc * esz;
+    const long long crow = remap ? (m0 / d->orow_div) * d->orow_stride : m0;
+    c.C = (char*)d->C + crow * d->ldc * esz;
     if (d->R) c.R = (const char*)d->R + m0 * d->ldr * 2;
     if (d->MIX) c.MIX = (const char*)d->MIX + m0 * d->ldmix * 2;
     if (d->rowbias) c.rowbias = d->rowbias + (m0 / d->rb_div) * d->ldrb;
-    c.orow_div = c.orow_stride = (int)mc;
+    if (!remap) c.orow_div = c.orow_stride = (int)mc;
     const int rc = acth_gemm(&c, stream);
     if (rc != ACTH_OK) return rc;
   }

@@ -23,6 +23,7 @@ Reference map (file:line under /root/reference/src/models/base unless noted):
 from __future__ import annotations
 
 import math
+import weakref
 import os
 from typing import List, Optional
 
@@ -363,13 +364,15 @@ def is_ip_processor(proc) -> bool:
 def _versioned_pack(mod: nn.Module, key, tensors, fn):
     """Kernel-layout pack cached on ``mod`` and keyed on the source tensors' in-place version counters,
     so a later ``load_state_dict`` into a foreign processor (the reference's ``load_adapter_states``)
-    invalidates it without any hook of ours."""
+    invalidates it without any hook of ours. The entry also holds weak references to the source tensors
+    themselves: a replaced Parameter (a fresh tensor that the caching allocator may place at the freed
+    address, with _version 0 again) never matches a stale entry."""
     cache = mod.__dict__.setdefault("_acth_vcache", {})
     ver = tuple((t.data_ptr(), t._version) for t in tensors)
     hit = cache.get(key)
-    if hit is None or hit[0] != ver:
+    if hit is None or hit[0] != ver or any(r() is not t for r, t in zip(hit[2], tensors)):
         with torch.no_grad():
-            hit = (ver, fn())
+            hit = (ver, fn(), tuple(weakref.ref(t) for t in tensors))
         cache[key] = hit
     return hit[1]
 

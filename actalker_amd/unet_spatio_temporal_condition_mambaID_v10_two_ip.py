@@ -266,7 +266,10 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         return model
 
     # -------------------------------------------------------------------------------- forward
-    def _prep_ctx(self, B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs):
+    def _prep_ctx(self, B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs,
+                  temb_only: bool = False):
+        """``temb_only``: the context of a shared CFG prefix (forward_tokens ``prefix_src``), which reads only
+        the ResBlock time-embedding projections -- the token projections are skipped."""
         dev = self.device
         ctx = Ctx(B, F, dev)
         if not torch.is_tensor(timestep):
@@ -303,7 +306,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         gate = cak.get("acth_gate")       # optional hint from actalker_amd.pipeline: exact-zero branches
         if gate is not None:
             ctx.audio_zero, ctx.vasa_zero = gate[0] == 0, gate[1] == 0
-        self._batched_ctx_projections(ctx)
+        self._batched_ctx_projections(ctx, temb_only)
         return ctx
 
     def _dev_ints(self, values, device) -> torch.Tensor:
@@ -316,7 +319,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             t = cache[key] = torch.tensor(values, dtype=torch.int64, device=device)
         return t
 
-    def _batched_ctx_projections(self, ctx):
+    def _batched_ctx_projections(self, ctx, temb_only: bool = False):
         """The per-call inputs every ResBlock / cross attention projects on its own -- ``temb`` through
         each ResBlock's ``time_emb_proj`` (diffusers resnet.py: ~40 per call), the ID token through each
         attn2's ``to_v`` (16 spatial on ``id_tok``, 16 temporal on ``id_mean``) -- as three GEMMs over the
@@ -341,7 +344,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         # the Mamba blocks' SiLU(ID / audio / VASA token projections) (mamba_layer.py:1955-1960), the rows
         # each branch places after its selected tokens: one GEMM per token kind, copied into place
         ctx.mamba_proj = {}
-        if mb:
+        if mb and not temb_only:
             groups = [("id", [m.id_proj for m in mb], ctx.id_tok)]
             if ctx.has_ip:
                 groups += [("audio", [m.audio_proj for m in mb], ctx.audio_tok),
@@ -372,6 +375,9 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         # IP-adapter audio K|V (to_k_ip[0] | to_v_ip[0]) and VASA V (to_v_ip[1]) of every IP attn2, on the
         # frame tokens (spatial) or the window means (temporal): the same concatenation
         ctx.ipkv, ctx.ipvb = {}, {}
+        ctx.vid = {}
+        if temb_only:
+            return
         if ctx.has_ip:
             for key, attns, atok, vtok in (("s", sp, ctx.audio_tok, ctx.vasa_tok),
                                            ("t", tp, ctx.audio_mean, ctx.vasa_mean)):
@@ -393,7 +399,6 @@ class UNetSpatioTemporalConditionModel(nn.Module):
                         n = sum(t.shape[0] for t in ws)
                         dst[id(a)] = out[:, o:o + n]
                         o += n
-        ctx.vid = {}
         for key, attns, tok in (("vid_s", sp, ctx.id_tok), ("vid_t", tp, ctx.id_mean)):
             if not attns:
                 continue
@@ -456,7 +461,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             t_u = timestep
             if torch.is_tensor(timestep) and timestep.numel() == B:
                 t_u = timestep.reshape(-1).index_select(0, ui.to(timestep.device))
-            ctx_u = self._prep_ctx(Bu, F, t_u, ehs_u, added_u, cross_attention_kwargs)
+            ctx_u = self._prep_ctx(Bu, F, t_u, ehs_u, added_u, cross_attention_kwargs, temb_only=True)
             prefix = (ctx_u, expand)
             x_in = take(x_tok, F * S0)
             rmap_in = take(spatial_condition_rmap, F) if spatial_condition_rmap is not None else None

@@ -240,6 +240,9 @@ class FamilyTimer:
             D = u.shape[1]
             return nb * L * D * 2 + nb * L * xdbl.shape[1] * 4 + 2 * nb * n_keep * D * 2
 
+        def w_scan2(a, b):
+            return sum(w_scan(**d) for d in (a, b))
+
         def w_gn(x, *a, x2=None, residual=None, **k):
             C = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
             return 2.0 * x.shape[0] * C * 2 + (x.shape[0] * C * 2 if residual is not None else 0)
@@ -254,6 +257,7 @@ class FamilyTimer:
         self._wrap(ops, "flash_attn", "flash_attn", w_flash)
         self._wrap(ops, "geglu_ffn", "geglu_ffn", w_ffn)
         self._wrap(ops, "selective_scan", "selective_scan", w_scan)
+        self._wrap(ops, "selective_scan2", "selective_scan", w_scan2)      # paired audio + expression launch
         self._wrap(ops, "groupnorm", "groupnorm", w_gn)
         self._wrap(ops, "layernorm", "layernorm", w_ln)
         mods.ops = ops
@@ -352,6 +356,9 @@ def main():
                     help="evaluate all 4 CFG branches even when two receive identical inputs (modes 0 / 1)")
     ap.add_argument("--no-four-branch-compare", action="store_true",
                     help="skip the extra timed run with all 4 CFG branches evaluated (reported beside the headline)")
+    ap.add_argument("--no-other-modes", action="store_true",
+                    help="skip the extra timed runs of the other BASELINE modes (C3 mode 1 / C4 mode 2 at N=1; "
+                         "reported beside the headline as other_modes)")
     ap.add_argument("--units-per-call", type=int, default=0,
                     help="(window, branch) units per UNet call; 0 = auto (fewest calls within the kernels' "
                          "2 GiB buffer extents; the reference's call is 4 units = 56 frames)")
@@ -469,6 +476,32 @@ def main():
         e4 = time.perf_counter() - t4
         four = dict(value=round(N / (cfg.num_inference_steps * e4 / args.steps), 4),
                     ms_per_step=round(1000.0 * e4 / args.steps, 2), cfg_branches_evaluated=4)
+    # the other BASELINE single-GPU configs (C3 mode 1, C4 mode 2 = C5's per-rank workload), timed after the
+    # headline on the same model: same loop settings, their own synthetic inputs / masks / gates
+    other = None
+    if world == 1 and not args.no_other_modes:
+        other = {}
+        for m in (0, 1, 2):
+            if m == args.mode:
+                continue
+            gate_m, name_m = MODES[m]
+            inp_m = synthetic_inputs(N, fpb, H, W, m)
+            be_m = pl.HipBackend(unet, H // 8, W // 8, inp_m["masks"], gate_m, inp_m["added"], N + fpb, fpb,
+                                 inp_m["image_latents"], inp_m["image_embeddings"], inp_m["audio_prompts"],
+                                 inp_m["vasa_prompts"], inp_m["pose_fea"])
+            tw_m = be_m.branch_twins() if cfg.dedup_branches else {}
+            with torch.no_grad():
+                pl.denoise(be_m, inp_m["latents"], cfg, rank, world, group, steps=1)
+            barrier()
+            tm = time.perf_counter()
+            with torch.no_grad():
+                out_m = pl.denoise(be_m, inp_m["latents"], cfg, rank, world, group, steps=args.steps)
+            barrier()
+            em = time.perf_counter() - tm
+            other[f"mode{m}"] = dict(workload=name_m, value=round(N / (cfg.num_inference_steps * em / args.steps), 4),
+                                     ms_per_step=round(1000.0 * em / args.steps, 2), steps=args.steps,
+                                     cfg_branches_evaluated=4 - len(tw_m), finite=bool(torch.isfinite(out_m).all()))
+            del be_m, inp_m, out_m
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(unet, H, W, frames=args.cpu_frames, mode=args.mode)
@@ -491,6 +524,7 @@ def main():
             "cfg_branches_evaluated": len(branches),
             "cfg_prefix_shared": cfg.share_cfg_prefix,
             "all_four_branches": four,
+            "other_modes": other,
             "finite": ok,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -67,10 +67,22 @@ def test_unet_full_geometry_matches_oracle(dev, full_unet, case):
                spatial_condition=pose.to(dev), cross_attention_kwargs={"ip_adapter_masks": masks},
                return_dict=False)[0]
     st = _stats(out, g["out"])
+    rpath = os.path.join(GOLD, f"unet_full_{case}_rounded.safetensors")
+    if os.path.exists(rpath):
+        # the fp16 budget (tools/gen_golden_fp16.py): the reference's shipped fp16 path (inference.yaml:66)
+        # modelled as the oracle with fp16 weights / op inputs / outputs, and the same model at bf16
+        rd = load_file(rpath)
+        st["fp16_ref_path_rel_l2"] = _stats(rd["fp16"], g["out"])["rel_l2"]
+        st["bf16_rounding_rel_l2"] = _stats(rd["bf16"], g["out"])["rel_l2"]
+        st["vs_fp16_ref_path_rel_l2"] = _stats(out, rd["fp16"])["rel_l2"]
     _log(f"unet_full_{case}", st)
     assert torch.isfinite(out).all()
     assert st["rel_l2"] < 2e-2, st
     assert st["max_abs"] < 0.25 * max(1.0, st["ref_rms"]), st
+    if "bf16_rounding_rel_l2" in st:
+        # stated tolerance: the HIP bf16 error stays within 1.5x of what bf16 rounding at op boundaries alone
+        # costs (fp16 rounding costs ~8x less: 3 more mantissa bits)
+        assert st["rel_l2"] < 1.5 * st["bf16_rounding_rel_l2"], st
 
 
 # ------------------------------------------------------------------------------------------ scan

@@ -352,7 +352,20 @@ def test_gemm_over_2gib(dev):
         ref_rows = (a[rows].float() @ w.float().t() + rowb[torch.arange(r0, r0 + 1000, device=dev) // RB]
                     + res[rows].float())
         assert rel(out[rows], ref_rows) < 1e-2, r0
-    del big, a, res, out
+    # output-row remap across the chunks (Mamba in_proj writing S-token images into L = S + 33 row
+    # slots, modules.SS2D_cond_v10): chunks are whole remap groups, C rebased by group
+    OD, OS = 9216, 9249
+    ngrp = -(-M // OD)
+    outr = torch.zeros(ngrp * OS, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(a, w, out=outr, orow=(OD, OS, 0))
+    chunk = ((1 << 30) - 65536) // (OD * LDA) * OD
+    for r0 in (0, chunk - 700, chunk, M - 1000):
+        src = torch.arange(r0, r0 + 1000, device=dev)
+        dst = (src // OD) * OS + src % OD
+        assert rel(outr[dst], a[r0:r0 + 1000].float() @ w.float().t()) < 1e-2, r0
+    pad = torch.arange(OD, OS, device=dev)                       # the slots between groups stay untouched
+    assert outr[pad].abs().max().item() == 0.0 and outr[pad + (ngrp - 1) * OS].abs().max().item() == 0.0
+    del big, a, res, out, outr
     torch.cuda.empty_cache()
     # conv: 190 images of 72 x 128 x 640 -> 2.24 GB of A
     B, H, W, Cin, Cout = 190, 72, 128, 640, 320

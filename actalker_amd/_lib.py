@@ -72,6 +72,40 @@ class IpAttnDesc(ctypes.Structure):
     ]
 
 
+class IpFoldDesc(ctypes.Structure):
+    _fields_ = [
+        ("kv", c_vp), ("ldkv", c_int),
+        ("wq", c_vp), ("ldwq", c_int),
+        ("wo", c_vp), ("ldwo", c_int),
+        ("bo", c_vp),
+        ("vid", c_vp), ("ldvid", c_int),
+        ("vb", c_vp), ("ldvb", c_int),
+        ("g2", c_vp), ("b2", c_vp),
+        ("kscale", c_float),
+        ("kp", c_vp), ("vp", c_vp),
+        ("gb", c_vp),
+        ("base", c_vp), ("vbw", c_vp),
+        ("nctx", c_int), ("C", c_int), ("H", c_int),
+    ]
+
+
+class XattnDesc(ctypes.Structure):
+    _fields_ = [
+        ("h", c_vp), ("ldh", c_int),
+        ("eps2", c_float),
+        ("kp", c_vp), ("vp", c_vp),
+        ("gb", c_vp),
+        ("base", c_vp), ("ldbase", c_int),
+        ("vbw", c_vp), ("ldvbw", c_int),
+        ("mask_a", c_vp), ("mask_b", c_vp),
+        ("sa", c_float), ("sb", c_float),
+        ("g3", c_vp), ("b3", c_vp), ("eps3", c_float),
+        ("out", c_vp), ("ldo", c_int),
+        ("n3", c_vp), ("ldn3", c_int),
+        ("M", c_int), ("C", c_int), ("H", c_int), ("rows_per_ctx", c_int), ("S", c_int),
+    ]
+
+
 class FfnDesc(ctypes.Structure):
     _fields_ = [
         ("x", c_vp), ("ldx", c_int),
@@ -155,6 +189,9 @@ SIGNATURES = {
     "acth_flash_attn": ([_P(AttnDesc), c_vp], c_int),
     "acth_temporal_attn": ([_P(TemporalAttnDesc), c_vp], c_int),
     "acth_ip_attn": ([_P(IpAttnDesc), c_vp], c_int),
+    "acth_ip_fold": ([_P(IpFoldDesc), c_vp], c_int),
+    "acth_xattn": ([_P(XattnDesc), c_vp], c_int),
+    "acth_debug_xattn_stamps": ([c_vp, c_int, c_int], c_int),
     "acth_layernorm": ([_P(LayerNormDesc), c_vp], c_int),
     "acth_im2col": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_int,
                      c_vp], c_int),

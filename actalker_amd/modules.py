@@ -102,6 +102,9 @@ def pack_ffn_w2(w: torch.Tensor) -> torch.Tensor:
 
 
 FUSED_FFN = os.environ.get("ACTH_FUSED_FFN", "1") != "0"
+# the fused IP-adapter cross attention block (acth_ip_fold + acth_xattn) where its shape allows; 0 = the
+# unfused norm2 / to_q / ip_attn / to_out / norm3 ops (A/B benchmarks, tests)
+FUSED_XATTN = os.environ.get("ACTH_FUSED_XATTN", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------
@@ -458,6 +461,51 @@ class Attention(Packed):
         return ops.gemm(comb, self.to_out[0].w(), bias=self.to_out[0].b(), residual=x_res)
 
 
+    # -- the fused form: norm2 -> cross attention (+ residual) -> norm3 in one kernel (acth_xattn), with to_q /
+    # to_out folded into the per-context audio keys / values (acth_ip_fold). Returns (h', norm3(h')) or None
+    # when the shape or processor is not one the fused kernel covers (the caller then runs the unfused ops).
+    def run_cross_fused(self, ctx: Ctx, h, S, temporal: bool, norm2, norm3):
+        M, C = h.shape
+        proc = self.processor
+        rows_per_ctx = ctx.F * S if temporal else S
+        if (not FUSED_XATTN or C not in ops.XATTN_C or not is_ip_processor(proc) or len(proc.to_k_ip) < 2
+                or rows_per_ctx % ops.XATTN_ROWS or M % rows_per_ctx or ctx.n_audio != 32 or C != self.heads * 64):
+            return None
+        if temporal:
+            id_tok, audio, vasa = ctx.id_mean, ctx.audio_mean, ctx.vasa_mean
+            ma = mb = None
+            use_a, use_b = not ctx.audio_zero, not ctx.vasa_zero
+        else:
+            id_tok, audio, vasa = ctx.id_tok, ctx.audio_tok, ctx.vasa_tok
+            ia, ib = ctx.mask(0, S), ctx.mask(1, S)
+            ma = None if (ia is None or ia.all_one) else ia.weights
+            mb = None if (ib is None or ib.all_one) else ib.weights
+            use_a = not ctx.audio_zero and not (ia is not None and ia.all_zero)
+            use_b = not ctx.vasa_zero and not (ib is not None and ib.all_zero)
+        if id_tok.shape[0] != M // rows_per_ctx:
+            return None
+        sa, sb = _scale_value(proc.scale[0]), _scale_value(proc.scale[1])
+        use_a, use_b = use_a and sa != 0.0, use_b and sb != 0.0
+        v_id = ctx.vid.get(id(self))
+        if v_id is None or v_id.shape[0] != id_tok.shape[0]:
+            v_id = ops.gemm(id_tok, self.to_v.w())
+        kv = vb = None
+        if use_a:
+            kv = ctx.ipkv.get(id(self))
+            if kv is None or kv.shape[0] != audio.shape[0]:
+                kv = ops.gemm(audio, ip_w_kv(proc, 0))
+        if use_b:
+            vb = ctx.ipvb.get(id(self))
+            if vb is None or vb.shape[0] != vasa.shape[0]:
+                vb = ops.gemm(vasa, ip_w_v(proc, 1))
+        woT = self.to_out[0]._pk("wT", lambda: _bf(self.to_out[0].weight.t()))
+        kp, vp, gb, base, vbw = ops.ip_fold(self.to_q.w(), woT, self.to_out[0].b(), v_id, kv=kv, vb=vb,
+                                            heads=self.heads, norm2=norm2.gb())
+        g3, b3 = norm3.gb()
+        return ops.xattn(h, norm2.eps, (g3, b3, norm3.eps), base, heads=self.heads,
+                         rows_per_ctx=rows_per_ctx, S=S, kp=kp, vp=vp, gb=gb, vbw=vbw, mask_a=ma, mask_b=mb, sa=sa, sb=sb)
+
+
 class GEGLU(Packed):
     def __init__(self, dim_in, dim_out, bias=True):
         super().__init__()
@@ -511,6 +559,10 @@ class BasicTransformerBlock(nn.Module):
         return self.attn1.run_self(ctx, n, h, S, temporal=False)
 
     def run_after_attn1(self, ctx: Ctx, h, S):
+        fused = self.attn2.run_cross_fused(ctx, h, S, False, self.norm2, self.norm3)
+        if fused is not None:
+            h, n = fused
+            return self.ff.run(n, h)
         n = ops.layernorm(h, *self.norm2.gb(), self.norm2.eps)
         h = self.attn2.run_cross(ctx, n, h, S, temporal=False)
         n = ops.layernorm(h, *self.norm3.gb(), self.norm3.eps, out=n)
@@ -540,6 +592,10 @@ class TemporalBasicTransformerBlock(nn.Module):
         del x
         n = ops.layernorm(t, *self.norm1.gb(), self.norm1.eps, out=n)
         t = self.attn1.run_self(ctx, n, t, S, temporal=True)
+        fused = self.attn2.run_cross_fused(ctx, t, S, True, self.norm2, self.norm3)
+        if fused is not None:
+            t, n = fused
+            return self.ff.run(n, t, mix=h_spatial, mix_alpha=mix_alpha)
         n = ops.layernorm(t, *self.norm2.gb(), self.norm2.eps, out=n)
         t = self.attn2.run_cross(ctx, n, t, S, temporal=True)
         n = ops.layernorm(t, *self.norm3.gb(), self.norm3.eps, out=n)

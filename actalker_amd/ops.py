@@ -241,6 +241,105 @@ def ip_attn(vbase: torch.Tensor, M: int, heads: int, rows_per_ctx: int, S: int, 
     return out
 
 
+XATTN_C = (320,)       # channel widths acth_xattn implements
+
+XATTN_ROWS = 64        # rows per workgroup: a context (frame / window) must be a multiple
+
+
+def ip_fold(wq: torch.Tensor, woT: torch.Tensor, bo: Optional[torch.Tensor], vid: torch.Tensor, *,
+            kv: Optional[torch.Tensor] = None, vb: Optional[torch.Tensor] = None, heads: int,
+            norm2=None, kscale: float = 1.4426950408889634 / 8.0):
+    """Fold the to_q / to_out projections of an IP-adapter attn2 into its per-context audio keys / values
+    (acth_ip_fold; ``woT`` = to_out[0].weight transposed, contiguous; ``norm2`` = (gamma, beta) of the LayerNorm
+    in front, folded in): returns (kp, vp, gb, base, vbw) -- K'' / V' (nctx*H*32, C) bf16 and the per-key LN2
+    constants gb (nctx*H*32, 2) fp32 (None without ``kv``), base = bo + Wo v_id and vbw = Wo v_vasa (nctx, C)
+    fp32 (vbw None without ``vb``)."""
+    lib = _lib.load()
+    C = wq.shape[0]
+    nctx = vid.shape[0]
+    for t, nm in ((wq, "wq"), (woT, "woT"), (vid, "vid")):
+        _need(t, torch.bfloat16, f"ip_fold {nm}")
+    if tuple(wq.shape) != (C, C) or tuple(woT.shape) != (C, C) or vid.shape[1] != C or heads * 64 != C:
+        raise _lib.ActhError(f"ip_fold: wq {tuple(wq.shape)} woT {tuple(woT.shape)} vid {tuple(vid.shape)} H={heads}")
+    d = _lib.IpFoldDesc()
+    d.wq, d.ldwq = wq.data_ptr(), _rows(wq, "ip_fold wq")
+    d.wo, d.ldwo = woT.data_ptr(), _rows(woT, "ip_fold woT")
+    if bo is not None:
+        _need(bo, torch.float32, "ip_fold bo")
+        d.bo = bo.data_ptr()
+    d.vid, d.ldvid = vid.data_ptr(), _rows(vid, "ip_fold vid")
+    base = torch.empty((nctx, C), device=vid.device, dtype=torch.float32)
+    d.base = base.data_ptr()
+    vbw = kp = vp = gb = None
+    if norm2 is not None:
+        d.g2, d.b2 = _p(norm2[0]), _p(norm2[1])
+    if vb is not None:
+        _need(vb, torch.bfloat16, "ip_fold vb")
+        if tuple(vb.shape) != (nctx, C):
+            raise _lib.ActhError(f"ip_fold: vb {tuple(vb.shape)} for {nctx} contexts")
+        d.vb, d.ldvb = vb.data_ptr(), _rows(vb, "ip_fold vb")
+        vbw = torch.empty((nctx, C), device=vid.device, dtype=torch.float32)
+        d.vbw = vbw.data_ptr()
+    if kv is not None:
+        _need(kv, torch.bfloat16, "ip_fold kv")
+        if kv.shape[0] != nctx * 32 or kv.shape[1] < 2 * C:
+            raise _lib.ActhError(f"ip_fold: kv {tuple(kv.shape)} for {nctx} contexts x 32 keys, C={C}")
+        d.kv, d.ldkv = kv.data_ptr(), _rows(kv, "ip_fold kv")
+        kp = torch.empty((nctx * heads * 32, C), device=vid.device, dtype=torch.bfloat16)
+        vp = torch.empty_like(kp)
+        gb = torch.empty((nctx * heads * 32, 2), device=vid.device, dtype=torch.float32)
+        d.kp, d.vp, d.gb = kp.data_ptr(), vp.data_ptr(), gb.data_ptr()
+    d.kscale = float(kscale)
+    d.nctx, d.C, d.H = nctx, C, heads
+    _lib.check(lib.acth_ip_fold(ctypes.byref(d), _stream()), "acth_ip_fold")
+    return kp, vp, gb, base, vbw
+
+
+def xattn(h: torch.Tensor, eps2: float, norm3, base: torch.Tensor, *, heads: int, rows_per_ctx: int, S: int,
+          kp: Optional[torch.Tensor] = None, vp: Optional[torch.Tensor] = None, gb: Optional[torch.Tensor] = None,
+          vbw: Optional[torch.Tensor] = None,
+          mask_a: Optional[torch.Tensor] = None, mask_b: Optional[torch.Tensor] = None, sa: float = 1.0,
+          sb: float = 1.0):
+    """Fused IP-adapter attn2 block (acth_xattn): returns (h + attn2(norm2(h)), norm3(that)).
+    ``eps2`` = norm2's eps (its weight / bias live in K'' / gb), ``norm3`` = (gamma fp32, beta fp32, eps);
+    K'' / V' / gb / base / vbw from :func:`ip_fold`."""
+    lib = _lib.load()
+    _need(h, torch.bfloat16, "xattn h")
+    M, C = h.shape
+    if C not in XATTN_C or M % rows_per_ctx or rows_per_ctx % XATTN_ROWS:
+        raise _lib.ActhError(f"xattn: M={M} C={C} rows_per_ctx={rows_per_ctx}")
+    nctx = M // rows_per_ctx
+    if tuple(base.shape) != (nctx, C) or (vbw is not None and tuple(vbw.shape) != (nctx, C)):
+        raise _lib.ActhError(f"xattn: base / vbw rows != {nctx} contexts")
+    if (kp is None) != (vp is None) or (kp is not None and (tuple(kp.shape) != (nctx * heads * 32, C) or gb is None
+                                                             or tuple(gb.shape) != (nctx * heads * 32, 2))):
+        raise _lib.ActhError("xattn: K'' / V' / gb missing or mis-shaped")
+    for m, nm in ((mask_a, "mask_a"), (mask_b, "mask_b")):
+        if m is not None:
+            _need(m, torch.float32, f"xattn {nm}")
+            if m.numel() < S:
+                raise _lib.ActhError(f"xattn: {nm} has {m.numel()} < S={S} entries")
+    out = torch.empty_like(h)
+    n3 = torch.empty_like(h)
+    d = _lib.XattnDesc()
+    d.h, d.ldh = h.data_ptr(), _rows(h, "xattn h")
+    g3, b3, e3 = norm3
+    d.eps2 = float(eps2)
+    d.g3, d.b3, d.eps3 = _p(g3), _p(b3), float(e3)
+    if kp is not None:
+        d.kp, d.vp, d.gb = kp.data_ptr(), vp.data_ptr(), gb.data_ptr()
+    d.base, d.ldbase = base.data_ptr(), _rows(base, "xattn base")
+    if vbw is not None:
+        d.vbw, d.ldvbw = vbw.data_ptr(), _rows(vbw, "xattn vbw")
+    d.mask_a, d.mask_b = _p(mask_a), _p(mask_b)
+    d.sa, d.sb = float(sa), float(sb)
+    d.out, d.ldo = out.data_ptr(), C
+    d.n3, d.ldn3 = n3.data_ptr(), C
+    d.M, d.C, d.H, d.rows_per_ctx, d.S = M, C, heads, rows_per_ctx, S
+    _lib.check(lib.acth_xattn(ctypes.byref(d), _stream()), "acth_xattn")
+    return out, n3
+
+
 # ------------------------------------------------------------------------------------------
 FFN_FUSED_C = (320,)   # channel widths acth_geglu_ffn implements
 

@@ -108,6 +108,54 @@ typedef struct ActhIpAttnDesc {
 } ActhIpAttnDesc;
 int acth_ip_attn(const ActhIpAttnDesc* d, hipStream_t stream);
 
+/* ---- fused IP-adapter cross attention block (attn2 of BasicTransformerBlock /
+ * TemporalBasicTransformerBlock with norm2 before and norm3 after, attention.py:223-343, 418-473;
+ * IPAdapterAttnProcessor2_0, attention_processor.py:2747-2934). Replaces, per call, the norm2 LayerNorm,
+ * the to_q GEMM, acth_ip_attn, the to_out GEMM (+ residual) and the norm3 LayerNorm:
+ *   out = h + bo + Wo (v_id + sa ma[s] softmax(q K^T / 8) V + sb mb[s] v_vasa),  q = Wq LN2(h)
+ *   n3  = LN3(out)
+ * LN2 itself folds in too: n . K'_j = rstd (h . (g2 o K'_j) - mu sum(g2 o K'_j)) + b2 . K'_j, so the kernel
+ * multiplies the raw rows of h and needs only their mean / variance.
+ * with Wq and Wo folded into per-context keys / values by acth_ip_fold (32 audio keys per head):
+ *   K'[ctx][h*32+j] = kscale * Wq_h^T k_{ctx,h,j},  V'[ctx][h*32+j] = Wo_h v_{ctx,h,j}   (C wide, bf16)
+ *   (Wo passed transposed, so every fold read is coalesced)
+ *   base[ctx] = bo + Wo v_id[ctx],  vbw[ctx] = Wo v_vasa[ctx]                              (fp32)
+ * Contexts are consecutive blocks of rows_per_ctx rows (a frame, or a window for the temporal block). */
+typedef struct ActhIpFoldDesc {
+  const void* kv; int ldkv;        /* (nctx*32, >= 2C) bf16 [K | V] of the audio tokens, or NULL (no audio term) */
+  const void* wq; int ldwq;        /* to_q.weight (C, C) bf16 */
+  const void* wo; int ldwo;        /* to_out[0].weight TRANSPOSED (C, C) bf16: wo[d][c] = Wo[c][d] */
+  const float* bo;                 /* to_out[0].bias (C) or NULL */
+  const void* vid; int ldvid;      /* (nctx, C) bf16: to_v(ID token) */
+  const void* vb; int ldvb;        /* (nctx, C) bf16: to_v_ip[1](VASA token), or NULL */
+  const float* g2; const float* b2; /* norm2 weight / bias (C) fp32, or NULL (1 / 0): folded into K'' / gb */
+  float kscale;                    /* folded into K' (log2(e) / 8: scores in exp2 units) */
+  void* kp; void* vp;              /* (nctx*H*32, C) bf16 outputs (kv != NULL): K'' = g2 o K', V' */
+  float* gb;                       /* (nctx*H*32, 2) fp32 output (kv != NULL): per key (sum_c K''_c, b2 . K') */
+  float* base; float* vbw;         /* (nctx, C) fp32 outputs; vbw written when vb != NULL */
+  int nctx, C, H;
+} ActhIpFoldDesc;
+int acth_ip_fold(const ActhIpFoldDesc* d, hipStream_t stream);
+
+typedef struct ActhXattnDesc {
+  const void* h; int ldh;          /* (M, C) bf16 residual stream */
+  float eps2;                      /* norm2 eps (its weight / bias are folded into kp / gb) */
+  const void* kp; const void* vp;  /* acth_ip_fold's K'' / V', or NULL (no audio term) */
+  const float* gb;                 /* acth_ip_fold's per-key LN2 constants (with kp) */
+  const float* base; int ldbase;   /* (nctx, C) fp32 */
+  const float* vbw; int ldvbw;     /* (nctx, C) fp32 or NULL (no VASA term) */
+  const float* mask_a; const float* mask_b;          /* per token position (period S) or NULL */
+  float sa, sb;
+  const float* g3; const float* b3; float eps3;      /* norm3 */
+  void* out; int ldo;              /* (M, C) bf16: h + attn2 */
+  void* n3; int ldn3;              /* (M, C) bf16: norm3(out) */
+  int M, C, H, rows_per_ctx, S;    /* C = 320 (level 0); rows_per_ctx % 64 == 0, M % rows_per_ctx == 0 */
+} ActhXattnDesc;
+int acth_xattn(const ActhXattnDesc* d, hipStream_t stream);
+/* diagnostics: host_dst == NULL -> enable (1) / disable (0) per-workgroup phase stamps; else copy the stamps
+ * of the first n_wgs workgroups (6 x u64 s_memtime each) of the last stamped launch */
+int acth_debug_xattn_stamps(unsigned long long* host_dst, int n_wgs, int enable);
+
 /* ---- LayerNorm with optional fused row-vector pre-add */
 typedef struct ActhLayerNormDesc {
   const void* x; int ldx;

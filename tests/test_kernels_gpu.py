@@ -480,6 +480,50 @@ def test_ip_attn(dev, masked, fps, nk, use_vb):
     assert rel(out2, vbase.float().repeat_interleave(rpc, 0)) < 5e-3
 
 
+@pytest.mark.parametrize("fps,masked,use_a,use_b", [(1, True, True, True), (1, False, True, False),
+                                                   (3, False, True, True), (1, True, False, True),
+                                                   (1, False, False, False)])
+def test_xattn_fused_block(dev, fps, masked, use_a, use_b):
+    """acth_ip_fold + acth_xattn: norm2 -> IP-adapter cross attention (ID + 32-key audio + VASA, per-token
+    masks) -> to_out + residual -> norm3 in one kernel, against torch fp32 of the unfused ops
+    (attention_processor.py:2747-2934 + attention.py:223-343). fps = frames per context (1: spatial attn2,
+    context = frame; 3: temporal attn2, context = window). C = 320, 5 heads; S = 256 tokens per frame."""
+    nctx, S, heads = 3, 256, 5
+    C = heads * 64
+    rpc = fps * S
+    M = nctx * rpc
+    h = bf(rnd(M, C, scale=2.0) + 0.5)
+    g2, b2, g3, b3 = 1 + 0.1 * rnd(C), 0.1 * rnd(C), 1 + 0.1 * rnd(C), 0.1 * rnd(C)
+    wq, wo = bf(rnd(C, C, scale=C ** -0.5)), bf(rnd(C, C, scale=C ** -0.5))
+    bo = 0.1 * rnd(C)
+    kv = bf(rnd(nctx * 32, 2 * C)) if use_a else None
+    vid = bf(rnd(nctx, C))
+    vb = bf(rnd(nctx, C)) if use_b else None
+    ma = torch.rand(S) if masked else None
+    mb = torch.rand(S) if masked else None
+    tod = lambda t: None if t is None else t.to(dev)   # noqa: E731
+    kp, vp, gb, base, vbw = ops.ip_fold(wq.to(dev), wo.t().contiguous().to(dev), bo.to(dev), vid.to(dev),
+                                        kv=tod(kv), vb=tod(vb), heads=heads, norm2=(g2.to(dev), b2.to(dev)))
+    out, n3 = ops.xattn(h.to(dev), 1e-5, (g3.to(dev), b3.to(dev), 1e-5), base, heads=heads, rows_per_ctx=rpc, S=S,
+                        kp=kp, vp=vp, gb=gb, vbw=vbw, mask_a=tod(ma), mask_b=tod(mb), sa=1.25, sb=0.75)
+    n = F.layer_norm(h.float(), (C,), g2, b2, 1e-5)
+    a = vid.float().repeat_interleave(rpc, 0)
+    if use_a:
+        q = (n @ wq.float().t()).view(nctx, rpc, heads, 64).transpose(1, 2)
+        kh = kv.float()[:, :C].view(nctx, 32, heads, 64).transpose(1, 2)
+        vh = kv.float()[:, C:].view(nctx, 32, heads, 64).transpose(1, 2)
+        o = F.scaled_dot_product_attention(q, kh, vh).transpose(1, 2).reshape(M, C)
+        wa = (ma if masked else torch.ones(S)).repeat(fps).repeat(nctx)[:, None]
+        a = a + 1.25 * wa * o
+    if use_b:
+        wb = (mb if masked else torch.ones(S)).repeat(fps).repeat(nctx)[:, None]
+        a = a + 0.75 * wb * vb.float().repeat_interleave(rpc, 0)
+    ref_out = h.float() + a @ wo.float().t() + bo
+    ref_n3 = F.layer_norm(ref_out, (C,), g3, b3, 1e-5)
+    assert rel(out, ref_out) < 1e-2, rel(out, ref_out)
+    assert rel(n3, ref_n3) < 1e-2, rel(n3, ref_n3)
+
+
 # ------------------------------------------------------------------------------------------ norms
 def test_layernorm_and_add(dev):
     M, C = 300, 640

@@ -115,6 +115,8 @@ class FfnDesc(ctypes.Structure):
         ("mix", c_vp), ("ldmix", c_int), ("mix_alpha", c_float),
         ("y", c_vp), ("ldy", c_int),
         ("M", c_int), ("C", c_int),
+        ("ln_g", c_vp), ("ln_b", c_vp), ("ln_eps", c_float), ("ln", c_int),
+        ("add", c_vp), ("ldadd", c_int), ("add_div", c_int),
     ]
 
 

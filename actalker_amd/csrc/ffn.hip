@@ -23,7 +23,11 @@
 //     piece) is the largest cost after the MFMAs -- the price of 128 tokens per weight pass, which is
 //     what the VGPR (x rows, O^T accumulators) and LDS (double-buffered chunks) budgets allow;
 //   * epilogue: O^T fragments -> per-wave LDS slab (token-major) -> + b2, residual, mix -> 16-byte
-//     row stores.
+//     row stores;
+//   * optional input LayerNorm (norm3 / norm_in, attention.py:330-331, 449-452) on the x rows in VGPRs:
+//     fp32 statistics (bf16 dot2) across the lane pair (hi = 0 / 1 hold the two channel halves), applied
+//     after the prologue barrier with gamma / beta from LDS -- the LN kernel's output write and the
+//     FFN's re-read of it leave HBM; optional frame-embedding row add (x + pos_emb[frame]) before it.
 // Numerics match the two-kernel path: fp32 accumulation, the gated hidden rounded to bf16 before the
 // down projection (as the GEGLU GEMM's bf16 output was); GELU by the degree-8 erf fit below.
 // LDS images (conflict-free ds_read_b128 of 32-row fragments for the gfx950 lane groups): W1 chunk
@@ -86,12 +90,13 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
   constexpr int NI1W = (NI1 + 7) / 8, NI2W = (NI2 + 7) / 8;
   constexpr int NS = KS + 2 * HF;         // MFMA slots per chunk iteration
   static_assert(C % 64 == 0 && W1CH % 8 == 0 && W1B % 1024 == 0 && W2B % 1024 == 0 && KS % 4 == 0, "shape");
-  static_assert(2 * (W1B + W2B + HXB) + (2 * I + C) * 4 <= 160 * 1024, "LDS");
+  static_assert(2 * (W1B + W2B + HXB) + (2 * I + 6 * C) * 4 <= 160 * 1024, "LDS");
   // Every buffer is its own LDS object and the chunk loop is unrolled by two so each access names
   // its buffer at compile time: the compiler then knows an LDS-DMA write into one buffer never
   // aliases a read of another and inserts no vmcnt(0) in front of fragment reads.
   __shared__ __attribute__((aligned(16))) char w1s0[W1B], w1s1[W1B], w2s0[W2B], w2s1[W2B], hxs0[HXB], hxs1[HXB];
-  __shared__ __attribute__((aligned(16))) float sb1[2 * I], sb2[C];
+  // sln: LayerNorm gamma | beta; sadd: the <= 3 add rows the workgroup's 128 tokens touch (add_div % 64 == 0)
+  __shared__ __attribute__((aligned(16))) float sb1[2 * I], sb2[C], sln[2 * C], sadd[3 * C];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -148,22 +153,87 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
   };
 
   // ---- this lane's token row of x as the up projection's B operand: k step ks holds channels
-  // 16 ks + 8 hi .. + 7
+  // 16 ks + 8 hi .. + 7 [+ the add row, rounded to bf16 as the stored sum; LayerNorm'd below]
   bf16x8_t xf[KS];
   {
-    const bf16_t* xr = (const bf16_t*)p.x + (size_t)(tok < p.M ? tok : 0) * p.ldx + 8 * hi;
+    const int tk = tok < p.M ? tok : 0;
+    const bf16_t* xr = (const bf16_t*)p.x + (size_t)tk * p.ldx + 8 * hi;
+    uint4 xv[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      uint4 v = *reinterpret_cast<const uint4*>(xr + 16 * ks);
-      if (tok >= p.M) v = make_uint4(0, 0, 0, 0);
-      xf[ks] = __builtin_bit_cast(bf16x8_t, v);
+    for (int ks = 0; ks < KS; ++ks) xv[ks] = *reinterpret_cast<const uint4*>(xr + 16 * ks);
+    const int ar0 = p.add ? blockIdx.x * 128 / p.add_div : 0;   // first add row of the workgroup
+    if (p.add) {
+      const int arl = (min(blockIdx.x * 128 + 127, p.M - 1)) / p.add_div;
+      for (int i = tid; i < 3 * C; i += 512) {
+        const int r = i / C, c = i - r * C;
+        sadd[i] = ar0 + r <= arl ? bf2f(((const bf16_t*)p.add)[(size_t)(ar0 + r) * p.ldadd + c]) : 0.0f;
+      }
     }
+    // the row loads, the bias / LN parameter staging and W1(0)'s DMA all in flight together: one memory
+    // latency for the prologue; the add / LayerNorm arithmetic runs once everything has landed
+    for (int i = tid; i < 2 * I; i += 512) sb1[i] = p.b1 ? p.b1[i] : 0.0f;
+    for (int i = tid; i < C; i += 512) sb2[i] = p.b2 ? p.b2[i] : 0.0f;
+    if (p.ln)
+      for (int i = tid; i < 2 * C; i += 512)
+        sln[i] = i < C ? (p.ln_g ? p.ln_g[i] : 1.0f) : (p.ln_b ? p.ln_b[i - C] : 0.0f);
+    stage_w1(0, std::false_type{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (p.add) {
+      const float* ar = sadd + (tk / p.add_div - ar0) * C + 8 * hi;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float x8[8];
+        unpack8(xv[ks], x8);
+        const float4 a0 = *reinterpret_cast<const float4*>(ar + 16 * ks);
+        const float4 a1 = *reinterpret_cast<const float4*>(ar + 16 * ks + 4);
+        x8[0] += a0.x; x8[1] += a0.y; x8[2] += a0.z; x8[3] += a0.w;
+        x8[4] += a1.x; x8[5] += a1.y; x8[6] += a1.z; x8[7] += a1.w;
+        xv[ks] = pack8(x8);                                  // rounded to bf16 as the stored sum
+      }
+    }
+    if (tok >= p.M)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xv[ks] = make_uint4(0, 0, 0, 0);
+    if (p.ln) {
+      // statistics over the lane pair's row (hi = 0 / 1 hold the two channel halves) by bf16 dot2 into fp32:
+      // sum and sum of squares straight from the packed row, no unpacked copy of it live (E[x^2] - mean^2,
+      // as the attention kernels' LayerNorms)
+      const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3f803f80u);
+      float sm = 0.0f, q = 0.0f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint32_t w[4] = {xv[ks].x, xv[ks].y, xv[ks].z, xv[ks].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x2_t v2 = __builtin_bit_cast(bf16x2_t, w[j]);
+          sm = __builtin_amdgcn_fdot2_f32_bf16(v2, one2, sm, false);
+          q = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, q, false);
+        }
+      }
+      sm += __shfl_xor(sm, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float mean = sm * (1.0f / C);
+      const float rstd = rsqrtf(fmaxf(q * (1.0f / C) - mean * mean, 0.0f) + p.ln_eps);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int c = 16 * ks + 8 * hi;
+        float x8[8];
+        unpack8(xv[ks], x8);
+        const float4 g0 = *reinterpret_cast<const float4*>(&sln[c]);
+        const float4 g1 = *reinterpret_cast<const float4*>(&sln[c + 4]);
+        const float4 b0 = *reinterpret_cast<const float4*>(&sln[C + c]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&sln[C + c + 4]);
+        const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x8[e] = fmaf((x8[e] - mean) * rstd, g[e], bb[e]);
+        xv[ks] = pack8(x8);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) xf[ks] = __builtin_bit_cast(bf16x8_t, xv[ks]);
   }
-  for (int i = tid; i < 2 * I; i += 512) sb1[i] = p.b1 ? p.b1[i] : 0.0f;
-  for (int i = tid; i < C; i += 512) sb2[i] = p.b2 ? p.b2[i] : 0.0f;
-  stage_w1(0, std::false_type{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   stamp(1);
 
   // O^T accumulators: fragment f holds channels half*C/2 + 32 f + 8 jb + 4 hi + r (register 4 jb + r)
@@ -287,7 +357,7 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
     constexpr int CPT = NFP * 4;                              // 8-channel chunks per token row
     constexpr int NCK = 32 * CPT / 64;                        // chunks per lane
     const int ch0 = half * (C / 2) + P * 64;
-    uint4 rr[NCK], mm[NCK];
+    uint4 rr[NCK], mm[NCK];                                 // mm: the mix row, or the add row (never both)
 #pragma unroll
     for (int k = 0; k < NCK; ++k) {
       const int ck = lane + 64 * k, tr = ck / CPT, c8 = (ck - tr * CPT) * 8;
@@ -295,6 +365,8 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
       rr[k] = p.res ? *reinterpret_cast<const uint4*>((const bf16_t*)p.res + (size_t)tk * p.ldres + ch0 + c8)
                     : make_uint4(0, 0, 0, 0);
       mm[k] = p.mix ? *reinterpret_cast<const uint4*>((const bf16_t*)p.mix + (size_t)tk * p.ldmix + ch0 + c8)
+            : p.add ? *reinterpret_cast<const uint4*>((const bf16_t*)p.add + (size_t)(tk / p.add_div) * p.ldadd +
+                                                      ch0 + c8)
                     : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -319,6 +391,13 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
       if (p.res) {
         float t[8];
         unpack8(rr[k], t);
+        if (p.add) {                                         // residual = bf16(res + add row), as stored
+          float a[8];
+          unpack8(mm[k], a);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] += a[e];
+          unpack8(pack8(t), t);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += t[e];
       }
@@ -346,6 +425,10 @@ extern "C" int acth_geglu_ffn(const ActhFfnDesc* d, hipStream_t stream) {
     return ACTH_EINVAL;
   if (((size_t)d->x | (size_t)d->y | (size_t)d->res | (size_t)d->mix | (size_t)d->w1 | (size_t)d->w2) & 15)
     return ACTH_EINVAL;
+  if (d->add && (d->mix || d->ldadd % 8 || d->ldadd < d->C || d->add_div <= 0 || d->add_div % 64 ||
+                 ((size_t)d->add & 15)))
+    return ACTH_EINVAL;
+  if (d->ln && !(d->ln_eps > 0.0f)) return ACTH_EINVAL;
   const long long w1_bytes = ((long long)(8 * d->C - 1) * d->ldw1 + d->C) * 2;
   const long long w2_bytes = ((long long)(d->C - 1) * d->ldw2 + 4 * d->C) * 2;
   if (w1_bytes >= 0x80000000LL || w2_bytes >= 0x80000000LL) return ACTH_EINVAL;

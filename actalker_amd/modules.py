@@ -105,6 +105,9 @@ FUSED_FFN = os.environ.get("ACTH_FUSED_FFN", "1") != "0"
 # the fused IP-adapter cross attention block (acth_ip_fold + acth_xattn) where its shape allows; 0 = the
 # unfused norm2 / to_q / ip_attn / to_out / norm3 ops (A/B benchmarks, tests)
 FUSED_XATTN = os.environ.get("ACTH_FUSED_XATTN", "1") != "0"
+# the blocks' "LayerNorm -> FeedForward" pairs (norm3 -> ff, norm_in (+ pos_emb) -> ff_in) as one kernel: the
+# LayerNorm runs in acth_geglu_ffn's prologue; 0 = a separate acth_layernorm pass (A/B benchmarks, tests)
+FUSED_FFN_LN = os.environ.get("ACTH_FUSED_FFN_LN", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------
@@ -501,8 +504,7 @@ class Attention(Packed):
         woT = self.to_out[0]._pk("wT", lambda: _bf(self.to_out[0].weight.t()))
         kp, vp, gb, base, vbw = ops.ip_fold(self.to_q.w(), woT, self.to_out[0].b(), v_id, kv=kv, vb=vb,
                                             heads=self.heads, norm2=norm2.gb())
-        g3, b3 = norm3.gb()
-        return ops.xattn(h, norm2.eps, (g3, b3, norm3.eps), base, heads=self.heads,
+        return ops.xattn(h, norm2.eps, None if norm3 is None else (*norm3.gb(), norm3.eps), base, heads=self.heads,
                          rows_per_ctx=rows_per_ctx, S=S, kp=kp, vp=vp, gb=gb, vbw=vbw, mask_a=ma, mask_b=mb, sa=sa, sb=sb)
 
 
@@ -539,6 +541,23 @@ class FeedForward(Packed):
         return ops.gemm(g, self.net[2].w(), bias=self.net[2].b(), residual=residual, mix=mix,
                         mix_alpha=mix_alpha)
 
+    def ln_fusable(self, C: int) -> bool:
+        return FUSED_FFN_LN and self.fusable(C)
+
+    def run_ln(self, x, ln, mix=None, mix_alpha: float = 0.0, add=None, add_div: int = 1):
+        """net[2](GEGLU(ln(x'))) + x' [AlphaBlender with ``mix``], x' = x [+ add[row // add_div]] -- the
+        blocks' "norm -> ff -> + residual" (attention.py:330-343, 449-457); one kernel at C = 320."""
+        if self.ln_fusable(x.shape[1]):
+            w, b = self.net[0].packed()
+            w2 = self._pk("w2perm", lambda: pack_ffn_w2(self.net[2].weight))
+            return ops.geglu_ffn(x, w, b, w2, self.net[2].b(), residual=x, mix=mix, mix_alpha=mix_alpha,
+                                 ln=(*ln.gb(), ln.eps), add=add, add_div=add_div)
+        if add is not None:
+            xs = torch.empty_like(x)
+            n = ops.layernorm(x, *ln.gb(), ln.eps, add=add, add_div=add_div, sum_out=xs)
+            return self.run(n, xs, mix=mix, mix_alpha=mix_alpha)
+        return self.run(ops.layernorm(x, *ln.gb(), ln.eps), x, mix=mix, mix_alpha=mix_alpha)
+
 
 class BasicTransformerBlock(nn.Module):
     def __init__(self, dim, num_attention_heads, attention_head_dim, cross_attention_dim=None):
@@ -559,14 +578,15 @@ class BasicTransformerBlock(nn.Module):
         return self.attn1.run_self(ctx, n, h, S, temporal=False)
 
     def run_after_attn1(self, ctx: Ctx, h, S):
-        fused = self.attn2.run_cross_fused(ctx, h, S, False, self.norm2, self.norm3)
+        ln3 = self.ff.ln_fusable(h.shape[1])
+        fused = self.attn2.run_cross_fused(ctx, h, S, False, self.norm2, None if ln3 else self.norm3)
         if fused is not None:
             h, n = fused
-            return self.ff.run(n, h)
+            return self.ff.run_ln(h, self.norm3) if n is None else self.ff.run(n, h)
         n = ops.layernorm(h, *self.norm2.gb(), self.norm2.eps)
         h = self.attn2.run_cross(ctx, n, h, S, temporal=False)
-        n = ops.layernorm(h, *self.norm3.gb(), self.norm3.eps, out=n)
-        return self.ff.run(n, h)
+        del n
+        return self.ff.run_ln(h, self.norm3)
 
 
 class TemporalBasicTransformerBlock(nn.Module):
@@ -586,20 +606,20 @@ class TemporalBasicTransformerBlock(nn.Module):
         """x = h + pos_emb[frame]; temporal block; AlphaBlender(h, x_temporal) fused in the last GEMM."""
         if not self.is_res:
             raise NotImplementedError("time_mix_inner_dim != dim is not used by the SVD UNet")
-        x = torch.empty_like(h_spatial)
-        n = ops.layernorm(h_spatial, *self.norm_in.gb(), self.norm_in.eps, add=pos_emb, add_div=S, sum_out=x)
-        t = self.ff_in.run(n, x)
-        del x
-        n = ops.layernorm(t, *self.norm1.gb(), self.norm1.eps, out=n)
+        t = self.ff_in.run_ln(h_spatial, self.norm_in, add=pos_emb, add_div=S)
+        n = ops.layernorm(t, *self.norm1.gb(), self.norm1.eps)
         t = self.attn1.run_self(ctx, n, t, S, temporal=True)
-        fused = self.attn2.run_cross_fused(ctx, t, S, True, self.norm2, self.norm3)
+        ln3 = self.ff.ln_fusable(t.shape[1])
+        fused = self.attn2.run_cross_fused(ctx, t, S, True, self.norm2, None if ln3 else self.norm3)
         if fused is not None:
             t, n = fused
+            if n is None:
+                return self.ff.run_ln(t, self.norm3, mix=h_spatial, mix_alpha=mix_alpha)
             return self.ff.run(n, t, mix=h_spatial, mix_alpha=mix_alpha)
         n = ops.layernorm(t, *self.norm2.gb(), self.norm2.eps, out=n)
         t = self.attn2.run_cross(ctx, n, t, S, temporal=True)
-        n = ops.layernorm(t, *self.norm3.gb(), self.norm3.eps, out=n)
-        return self.ff.run(n, t, mix=h_spatial, mix_alpha=mix_alpha)
+        del n
+        return self.ff.run_ln(t, self.norm3, mix=h_spatial, mix_alpha=mix_alpha)
 
 
 # ------------------------------------------------------------------------------------------

@@ -301,7 +301,8 @@ def xattn(h: torch.Tensor, eps2: float, norm3, base: torch.Tensor, *, heads: int
           mask_a: Optional[torch.Tensor] = None, mask_b: Optional[torch.Tensor] = None, sa: float = 1.0,
           sb: float = 1.0):
     """Fused IP-adapter attn2 block (acth_xattn): returns (h + attn2(norm2(h)), norm3(that)).
-    ``eps2`` = norm2's eps (its weight / bias live in K'' / gb), ``norm3`` = (gamma fp32, beta fp32, eps);
+    ``eps2`` = norm2's eps (its weight / bias live in K'' / gb), ``norm3`` = (gamma fp32, beta fp32, eps), or
+    None when the consumer (geglu_ffn's ``ln``) normalises itself -- then the second result is None;
     K'' / V' / gb / base / vbw from :func:`ip_fold`."""
     lib = _lib.load()
     _need(h, torch.bfloat16, "xattn h")
@@ -320,12 +321,13 @@ def xattn(h: torch.Tensor, eps2: float, norm3, base: torch.Tensor, *, heads: int
             if m.numel() < S:
                 raise _lib.ActhError(f"xattn: {nm} has {m.numel()} < S={S} entries")
     out = torch.empty_like(h)
-    n3 = torch.empty_like(h)
+    n3 = None if norm3 is None else torch.empty_like(h)
     d = _lib.XattnDesc()
     d.h, d.ldh = h.data_ptr(), _rows(h, "xattn h")
-    g3, b3, e3 = norm3
     d.eps2 = float(eps2)
-    d.g3, d.b3, d.eps3 = _p(g3), _p(b3), float(e3)
+    if norm3 is not None:
+        g3, b3, e3 = norm3
+        d.g3, d.b3, d.eps3 = _p(g3), _p(b3), float(e3)
     if kp is not None:
         d.kp, d.vp, d.gb = kp.data_ptr(), vp.data_ptr(), gb.data_ptr()
     d.base, d.ldbase = base.data_ptr(), _rows(base, "xattn base")
@@ -334,7 +336,8 @@ def xattn(h: torch.Tensor, eps2: float, norm3, base: torch.Tensor, *, heads: int
     d.mask_a, d.mask_b = _p(mask_a), _p(mask_b)
     d.sa, d.sb = float(sa), float(sb)
     d.out, d.ldo = out.data_ptr(), C
-    d.n3, d.ldn3 = n3.data_ptr(), C
+    if n3 is not None:
+        d.n3, d.ldn3 = n3.data_ptr(), C
     d.M, d.C, d.H, d.rows_per_ctx, d.S = M, C, heads, rows_per_ctx, S
     _lib.check(lib.acth_xattn(ctypes.byref(d), _stream()), "acth_xattn")
     return out, n3
@@ -347,9 +350,12 @@ FFN_FUSED_C = (320,)   # channel widths acth_geglu_ffn implements
 def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p: torch.Tensor,
               b2: Optional[torch.Tensor], *, residual: Optional[torch.Tensor] = None,
               mix: Optional[torch.Tensor] = None, mix_alpha: float = 0.0,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Fused FeedForward(geglu): y = [a*mix + (1-a)*](W2 (h*gelu(g)) + b2 [+ residual]).
-    ``w1``/``b1`` from modules.pack_geglu, ``w2p`` from modules.pack_ffn_w2."""
+              out: Optional[torch.Tensor] = None, ln=None, add: Optional[torch.Tensor] = None,
+              add_div: int = 1) -> torch.Tensor:
+    """Fused FeedForward(geglu): y = [a*mix + (1-a)*](W2 (h*gelu(g)) + b2 [+ residual]), [h | g] = W1 x' + b1.
+    ``w1``/``b1`` from modules.pack_geglu, ``w2p`` from modules.pack_ffn_w2. ``ln`` = (gamma, beta, eps):
+    x' = LayerNorm(x) computed in the kernel (else x' = x). ``add`` (rows, C) bf16: x and the residual each
+    get bf16(. + add[row // add_div]) first (not with ``mix``)."""
     lib = _lib.load()
     _need(x, torch.bfloat16, "geglu_ffn x")
     M, C = x.shape
@@ -383,6 +389,18 @@ def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p
         d.mix, d.ldmix, d.mix_alpha = mix.data_ptr(), _rows(mix, "geglu_ffn mix"), float(mix_alpha)
     d.y, d.ldy = out.data_ptr(), _rows(out, "geglu_ffn out")
     d.M, d.C = M, C
+    if ln is not None:
+        g, b, eps = ln
+        for t in (g, b):
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != C):
+                raise _lib.ActhError("geglu_ffn ln: gamma / beta must be contiguous fp32 of C entries")
+        d.ln_g, d.ln_b, d.ln_eps, d.ln = _p(g), _p(b), float(eps), 1
+    if add is not None:
+        _need(add, torch.bfloat16, "geglu_ffn add")
+        if mix is not None or add_div <= 0 or add_div % 64 or add.dim() != 2 or add.shape[1] < C or \
+                add.shape[0] * add_div < M:
+            raise _lib.ActhError(f"geglu_ffn add: {tuple(add.shape)} add_div={add_div} for M={M}")
+        d.add, d.ldadd, d.add_div = add.data_ptr(), _rows(add, "geglu_ffn add"), int(add_div)
     _lib.check(lib.acth_geglu_ffn(ctypes.byref(d), _stream()), "acth_geglu_ffn")
     return out
 

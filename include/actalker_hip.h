@@ -69,6 +69,13 @@ typedef struct ActhFfnDesc {
   const void* mix; int ldmix; float mix_alpha;
   void* y; int ldy;
   int M, C;
+  /* optional fused input LayerNorm (ln != 0): the kernel normalises x per token (fp32 statistics by bf16 dot2,
+   * ln_g / ln_b may be NULL = 1 / 0) before the up projection -- norm3 / norm_in of the block folded into
+   * the FFN, so the normalised tensor never reaches HBM. Optional row vector add (add != NULL):
+   * x <- bf16(x + add[row / add_div]) (add_div % 64 == 0) before the LayerNorm, and res <- bf16(res + add[row / add_div]) in the
+   * epilogue (TemporalBasicTransformerBlock's "h + pos_emb" feeding norm_in and the ff_in residual). */
+  const float* ln_g; const float* ln_b; float ln_eps; int ln;
+  const void* add; int ldadd; int add_div;
 } ActhFfnDesc;
 int acth_geglu_ffn(const ActhFfnDesc* d, hipStream_t stream);
 /* diagnostics: host_dst == NULL -> enable (1) / disable (0) per-workgroup phase stamps; else copy the

@@ -128,6 +128,46 @@ def test_geglu_ffn_fused(dev, M, case):
     assert rel(out, two) < 4e-3
 
 
+@pytest.mark.parametrize("M,case", [(1, "ln"), (300, "ln_mix"), (4133, "ln_add"), (2 * 128 * 7 + 5, "ln"),
+                                    (14 * 64, "ln_add")])
+def test_geglu_ffn_fused_layernorm(dev, M, case):
+    """acth_geglu_ffn with its prologue LayerNorm (norm3 -> ff, norm_in (+ pos_emb) -> ff_in): y = FFN(LN(x')) +
+    x' [mix], x' = bf16(x + add[row // div]); against torch fp32 and against layernorm + geglu_ffn. The rows carry
+    a common offset (the statistics must remove it); the residual is subtracted before the comparison so the
+    FFN term is what the tolerance measures."""
+    from actalker_amd.modules import pack_geglu, pack_ffn_w2
+    C, inner, div = 320, 1280, 64
+    x = bf(rnd(M, C) + 3.0)
+    g3, b3 = 1.0 + 0.2 * rnd(C), 0.1 * rnd(C)
+    w1 = rnd(2 * inner, C, scale=C ** -0.5)
+    b1 = rnd(2 * inner, scale=0.1)
+    w2 = rnd(C, inner, scale=inner ** -0.5)
+    b2 = rnd(C, scale=0.1)
+    add = bf(rnd((M + div - 1) // div, C)) if case == "ln_add" else None
+    mix = bf(rnd(M, C)) if case == "ln_mix" else None
+    wp, bp = pack_geglu(w1, b1)
+    w2p = pack_ffn_w2(w2)
+    dv = lambda t: None if t is None else t.to(dev)
+    xd = x.to(dev)
+    out = ops.geglu_ffn(xd, wp.to(dev), bp.to(dev), w2p.to(dev), b2.to(dev), residual=xd, mix=dv(mix),
+                        mix_alpha=0.3, ln=(g3.to(dev), b3.to(dev), 1e-5), add=dv(add), add_div=div)
+    xs = x.float() if add is None else bf(x.float() + add.float().repeat_interleave(div, 0)[:M]).float()
+    n = bf(F.layer_norm(xs, (C,), g3, b3, 1e-5)).float()
+    h, g = (n @ bf(w1).float().t() + b1).chunk(2, -1)
+    refo = bf(h * F.gelu(g)).float() @ bf(w2).float().t() + b2 + xs
+    base = xs if mix is None else 0.3 * mix.float() + 0.7 * xs
+    if mix is not None:
+        refo = 0.3 * mix.float() + 0.7 * refo
+    assert rel(out.float().cpu() - base, refo - base) < 1e-2
+    # the unfused pair: acth_layernorm (+ row add, sum out) then acth_geglu_ffn
+    xs_d = torch.empty_like(xd)
+    nd = ops.layernorm(xd, g3.to(dev), b3.to(dev), 1e-5, add=dv(add), add_div=div,
+                       sum_out=xs_d if add is not None else None)
+    two = ops.geglu_ffn(nd, wp.to(dev), bp.to(dev), w2p.to(dev), b2.to(dev),
+                        residual=xs_d if add is not None else xd, mix=dv(mix), mix_alpha=0.3)
+    assert rel(out.float().cpu() - base, two.float().cpu() - base) < 4e-3
+
+
 def test_geglu_ffn_rejects_bad_shapes(dev):
     from actalker_amd import _lib
     x = torch.zeros(8, 640, device=dev, dtype=torch.bfloat16)
@@ -522,6 +562,10 @@ def test_xattn_fused_block(dev, fps, masked, use_a, use_b):
     ref_n3 = F.layer_norm(ref_out, (C,), g3, b3, 1e-5)
     assert rel(out, ref_out) < 1e-2, rel(out, ref_out)
     assert rel(n3, ref_n3) < 1e-2, rel(n3, ref_n3)
+    # norm3 left to the feed-forward kernel: the same h', no n3
+    out2, none = ops.xattn(h.to(dev), 1e-5, None, base, heads=heads, rows_per_ctx=rpc, S=S,
+                           kp=kp, vp=vp, gb=gb, vbw=vbw, mask_a=tod(ma), mask_b=tod(mb), sa=1.25, sb=0.75)
+    assert none is None and torch.equal(out2, out)
 
 
 # ------------------------------------------------------------------------------------------ norms

@@ -2,7 +2,10 @@
 entry, after the prologue (x rows in VGPRs, W1 chunk 0 in LDS), after chunk 0, after chunks 10 and 30,
 after the chunk loop, after the epilogue. Prints mean cycles per phase and per chunk.
 
-  python tools/ffn_stamps.py [--M 774144]
+  python tools/ffn_stamps.py [--M 774144] [--modes plain,ln,ln_add,ln_mix]
+
+Modes: plain = residual; ln = the prologue LayerNorm with residual = x (norm3 -> ff); ln_add = also the
+frame-embedding row add (norm_in + pos_emb -> ff_in); ln_mix = ln with the AlphaBlender mix (temporal ff).
 """
 import argparse
 import ctypes
@@ -20,10 +23,16 @@ from actalker_amd.modules import pack_ffn_w2, pack_geglu  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=774144)
+    ap.add_argument("--modes", default="plain,ln,ln_add,ln_mix")
     a = ap.parse_args()
+    for mode in a.modes.split(","):
+        one(a.M, mode)
+
+
+def one(M, mode):
     dev = torch.device("cuda:0")
     lib = _lib.load()
-    C, M = 320, a.M
+    C = 320
     g = torch.Generator().manual_seed(0)
     x = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
     res = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
@@ -32,9 +41,16 @@ def main():
     w1, b1, w2 = w1.to(dev), b1.to(dev), w2.to(dev)
     b2 = torch.zeros(C, device=dev)
     out = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    ln = (1.0 + 0.1 * torch.randn(C, generator=g)).to(dev), (0.1 * torch.randn(C, generator=g)).to(dev), 1e-5
+    S = 9216
+    emb = torch.randn((M + S - 1) // S, C, generator=g).to(dev, torch.bfloat16)
 
     def run():
-        ops.geglu_ffn(x, w1, b1, w2, b2, residual=res, out=out)
+        if mode == "plain":
+            ops.geglu_ffn(x, w1, b1, w2, b2, residual=res, out=out)
+        else:
+            ops.geglu_ffn(x, w1, b1, w2, b2, residual=x, out=out, ln=ln, add=emb if mode == "ln_add" else None,
+                          add_div=S, mix=res if mode == "ln_mix" else None, mix_alpha=0.3)
 
     for _ in range(3):
         run()
@@ -60,7 +76,7 @@ def main():
     tot = st[:, 6] - st[:, 0]
     names = ["prologue", "chunk0", "chunks1-10", "chunks11-30", "chunks31-40", "epilogue"]
     per = [1, 1, 10, 20, 10, 1]
-    print(f"M={M}: {ms:.3f} ms; {len(st)} WGs stamped; mean cycles/WG total {tot.mean():.0f} "
+    print(f"[{mode}] M={M}: {ms:.3f} ms; {len(st)} WGs stamped; mean cycles/WG total {tot.mean():.0f} "
           f"(median {np.median(tot):.0f}, p90 {np.percentile(tot, 90):.0f})")
     for i, nm in enumerate(names):
         print(f"  {nm:12s} {d[:, i].mean():9.0f}  per chunk {d[:, i].mean() / per[i]:8.0f}  "

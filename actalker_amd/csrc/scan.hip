@@ -499,6 +499,254 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// scan_quad_kernel: the fused SS2D scan (G = 2 directions over the same u, direction 1 reversed) on
+// bf16 xdbl rows -- the reference's x_dbl dtype (mamba_layer.py:1521: einsum of the half-precision xs
+// and x_proj_weight; B / C go to selective_scan_fn in that dtype) -- laid out per direction as
+// [dt (R rounded up to 4) | B (16) | C (16)].
+//
+// Lane layout. Wave w of the block owns channels dbase + 16 w + j (j = lane & 15); lane group
+// g = lane >> 4 holds states 4g .. 4g+3 of channel j (h[r] = h[state 4g + r][channel j]). That is the
+// accumulator layout of a 16x16 MFMA with rows = states, columns = channels, so
+//  * the input term (dt u)_t[d] B_t[n] of four tokens is ONE v_mfma_f32_16x16x1_4b_f32: four 16x16
+//    rank-1 outer products B_t (x) (dt u)_t, fp32 operands and products (exact, as the fmaf it
+//    replaces), on the matrix core instead of 4 VALU multiplies per lane and token;
+//  * delta (dt_proj + dt_bias + softplus) of a 16-token tile is a v_mfma_f32_16x16x4_f32 chain with the
+//    tile's dt columns as A (rows = tokens) and dt_w as B (columns = channels): lane (g, j) receives
+//    tokens 4g..4g+3 of its own channel j and parks them in LDS for the channel's four lane groups;
+//  * the readout y_t[d] = sum_n C_t[n] h_t[n][d] is 4 FMAs per lane and token, then the four lane
+//    groups are summed for 4 tokens at once: 2 v_permlane32_swap + 1 v_permlane16_swap + 3 adds
+//    (a reduce-scatter: lane group g ends with token tau(g) = [0, 2, 1, 3][g] of the quad).
+// What stays on the VALU per lane and token: 4 x (dt * A, exp2, state FMA, readout FMA) + ~1.5
+// (reduction, D skip, conversions) -- the old layout's per-(state, token) dt u B multiply is gone, and
+// plain f32 ops issue at ~0.55 of the cost of packed ones on gfx950 (tools/probes/valu_probe.hip).
+// Forward direction stops at n_keep: tokens past the last kept output (ID / condition tokens) only feed
+// a state nobody reads. Blocks are dealt XCD-major (the channel blocks of one (batch, direction) share
+// their xdbl tiles through one L2).
+#ifndef SQ_CH
+#define SQ_CH 64              // channels per block (16 per wave)
+#endif
+#define SQ_NT (SQ_CH * 4)
+#ifndef SQ_OCC
+#define SQ_OCC 5              // waves per SIMD the register budget targets (R <= 40)
+#endif
+#ifndef SQ_PF
+#define SQ_PF 2               // tiles of global loads in flight (register ring)
+#endif
+#ifndef SQ_FENCE
+#define SQ_FENCE 0
+#endif
+// one token's exps / C reads are not hoisted above the previous token's (register budget for occupancy)
+#if SQ_FENCE
+#define SQ_TOKEN_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SQ_TOKEN_FENCE() do {} while (0)
+#endif
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+#define SQ_UP (SQ_CH + 16)    // u / y tile row in bf16: 4 token rows land on disjoint banks
+
+template <int R, bool SOFTPLUS>
+__global__ __launch_bounds__(SQ_NT, R <= 40 ? SQ_OCC : SQ_OCC - 1) void scan_quad_kernel(const ActhScanDesc p0,
+                                                                           const ActhScanDesc p1, int nb0, int gx) {
+  constexpr int R4 = (R + 3) & ~3;
+  constexpr int KS = R4 / 4;
+  constexpr int W = R4 + 32;                              // bf16 per token and direction in xdbl
+  constexpr int WP = ((W / 4) % 2 == 0) ? W + 4 : W;      // LDS row in floats: odd 16-byte count
+  constexpr int DLP = 20;                                 // delta row per channel: 16 tokens + pad
+  constexpr int XQ = W / 4;                               // 8-byte chunks per token row
+  constexpr int XN = (16 * XQ + SQ_NT - 1) / SQ_NT;       // xdbl chunks per thread
+  __shared__ __attribute__((aligned(16))) float xs[16 * WP];
+  __shared__ __attribute__((aligned(16))) bf16_t us[16 * SQ_UP];
+  __shared__ __attribute__((aligned(16))) bf16_t ys[16 * SQ_UP];
+  __shared__ __attribute__((aligned(16))) float dls[SQ_CH * DLP];
+  __shared__ float wls[SQ_CH * (R4 + 1)];
+
+  // XCD-major block order (bijective for any grid size; hardware deals block P to XCD P % 8)
+  const unsigned P = blockIdx.x, NB = gridDim.x;
+  const unsigned xcd = P & 7, q8 = NB >> 3, r8 = NB & 7;
+  const unsigned wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (P >> 3);
+  const int bx = (int)(wg % (unsigned)gx), kz = (int)(wg / (unsigned)gx);
+  const int k = kz & 1, z = kz >> 1;
+  const bool second = z >= nb0;
+  const ActhScanDesc& p = *(second ? &p1 : &p0);
+  const int b = z - (second ? nb0 : 0);
+
+  const int t = threadIdx.x, ln = t & 63, w = t >> 6, g = ln >> 4, j = ln & 15;
+  const int dbase = bx * SQ_CH;
+  const int ch = dbase + 16 * w + j;
+  const bool active = ch < p.D;
+  const int cc = active ? ch : 0;
+  const bool rev = k == 1;
+  const int Lend = rev ? p.L : p.n_keep;
+
+  // delta MFMA B operand dt_w[k][ch][4s + g], parked in LDS (wave-local rows) rather than KS registers
+  float* wlw = wls + (16 * w + j) * (R4 + 1);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int r = 4 * s + g;
+    wlw[4 * s + g] = (r < R && active) ? p.dt_w[((size_t)k * p.D + cc) * R + r] : 0.0f;
+  }
+  const float dtb = (p.dt_b && active) ? p.dt_b[k * p.D + cc] : 0.0f;
+  float a2[4], h[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    a2[r] = -__expf(p.A_log[((size_t)k * p.D + cc) * 16 + 4 * g + r]) * 1.4426950408889634f;
+    h[r] = 0.0f;
+  }
+  const float dsk = (p.Dskip && active) ? p.Dskip[k * p.D + cc] : 0.0f;
+
+  const bf16_t* ub = (const bf16_t*)p.u + (size_t)b * p.L * p.ldu + dbase;
+  const bf16_t* xb = (const bf16_t*)p.xdbl + (size_t)b * p.L * p.ldx + k * W;
+  bf16_t* yb = (p.y1 && k == 1) ? (bf16_t*)p.y1 : (bf16_t*)p.y0 + (size_t)k * p.y_gstride;
+  yb += (size_t)b * p.n_keep * p.ldy + dbase;
+  auto pos_of = [&](int i) { return rev ? p.L - 1 - i : i; };
+  // Branch-free global traffic: buffer loads / stores whose masked-off lanes carry an out-of-range offset
+  // (loads return 0, stores are dropped), so every tile issues the same memory ops and the compiler's
+  // s_waitcnt keeps the ring's younger loads (and the previous tile's y stores) in flight.
+  const unsigned OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(xb), (short)0,
+                                                                      (int)((size_t)p.L * p.ldx * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(ub), (short)0,
+                                                                      (int)((size_t)p.L * p.ldu * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(yb, (short)0,
+                                                                      (int)((size_t)p.n_keep * p.ldy * 2), 0x00020000);
+
+  // global -> register prefetch ring of SQ_PF tiles (slots are compile-time: the tile loop is unrolled by SQ_PF)
+  uint2 px[SQ_PF][XN], pu[SQ_PF];
+  const int ut = t / (SQ_CH / 4), uc = (t % (SQ_CH / 4)) * 4;   // this thread's u / y chunk: token, channel
+  auto prefetch = [&](auto slot, int i0) {
+    constexpr int S = decltype(slot)::value;
+#pragma unroll
+    for (int e = 0; e < XN; ++e) {                        // xdbl chunk idx: token idx / XQ, column 4 (idx % XQ)
+      const int idx = t + e * SQ_NT, xt = idx / XQ, xc = (idx - xt * XQ) * 4;
+      const bool ok = xt < 16 && i0 + xt < Lend;
+      const unsigned off = ok ? (unsigned)(pos_of(i0 + xt) * p.ldx + xc) * 2u : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rx, (int)off, 0, 0);
+      px[S][e] = make_uint2(v[0], v[1]);
+    }
+    const bool ok = i0 + ut < Lend && dbase + uc < p.D;
+    const unsigned off = ok ? (unsigned)(pos_of(i0 + ut) * p.ldu + uc) * 2u : OOB;
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(ru, (int)off, 0, 0);
+    pu[S] = make_uint2(v[0], v[1]);
+  };
+  auto commit = [&](auto slot) {
+    constexpr int S = decltype(slot)::value;
+#pragma unroll
+    for (int e = 0; e < XN; ++e) {
+      const int idx = t + e * SQ_NT, xt = idx / XQ, xc = (idx - xt * XQ) * 4;
+      if (xt < 16)
+        *reinterpret_cast<float4*>(&xs[xt * WP + xc]) =
+            make_float4(__uint_as_float(px[S][e].x << 16), __uint_as_float(px[S][e].x & 0xffff0000u),
+                        __uint_as_float(px[S][e].y << 16), __uint_as_float(px[S][e].y & 0xffff0000u));
+    }
+    *reinterpret_cast<uint2*>(&us[ut * SQ_UP + uc]) = pu[S];
+  };
+
+  float* dlw = dls + (16 * w + j) * DLP;                  // this channel's delta row (wave-local)
+  const int tg = ((g & 1) << 1) | (g >> 1);               // token of the quad this lane group ends with
+  const f32x16_t zero16 = {};
+
+  // quad q (tokens 4q..4q+3 of the tile): per token the input term dt u B of the lane's 4 states is one
+  // v_mfma_f32_4x4x1_16b_f32 (lane l gets A(lane 4(l >> 2) + r) x B(lane l), r = 0..3: with A = B_t[4g + (j & 3)]
+  // and B = (dt u)_t[j] that is B_t[4g + r] (dt u)_t[j], exactly this lane's states)
+  const float dsk0 = g == 0 ? dsk : 0.0f;                 // D u added once per channel (lane group 0)
+  auto quad = [&](int q) {
+    const float4 dt4 = *reinterpret_cast<const float4*>(dlw + 4 * q);
+    const float dts[4] = {dt4.x, dt4.y, dt4.z, dt4.w};
+    float pp[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int tt = 4 * q + s;
+      const float us_ = bf2f(us[tt * SQ_UP + 16 * w + j]);
+      const f32x4_t db = __builtin_amdgcn_mfma_f32_4x4x1f32(xs[tt * WP + R4 + 4 * g + (j & 3)], dts[s] * us_,
+                                                            (f32x4_t){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const float4 cv = *reinterpret_cast<const float4*>(&xs[tt * WP + R4 + 16 + 4 * g]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[r] = fmaf(fast_exp2(dts[s] * a2[r]), h[r], db[r]);
+      pp[s] = fmaf(h[3], cv.w, fmaf(h[2], cv.z, fmaf(h[1], cv.y, fmaf(h[0], cv.x, dsk0 * us_))));
+      SQ_TOKEN_FENCE();
+    }
+    // sum the four lane groups: lane group g ends with token tau(g)
+    const auto sa = __builtin_amdgcn_permlane32_swap(__float_as_uint(pp[0]), __float_as_uint(pp[1]), false, false);
+    const auto sb = __builtin_amdgcn_permlane32_swap(__float_as_uint(pp[2]), __float_as_uint(pp[3]), false, false);
+    const float ra = __uint_as_float(sa[0]) + __uint_as_float(sa[1]);
+    const float rb = __uint_as_float(sb[0]) + __uint_as_float(sb[1]);
+    const auto sc = __builtin_amdgcn_permlane16_swap(__float_as_uint(ra), __float_as_uint(rb), false, false);
+    ys[(4 * q + tg) * SQ_UP + 16 * w + j] = f2bf(__uint_as_float(sc[0]) + __uint_as_float(sc[1]));
+  };
+
+  auto tile = [&](int i0, auto slot) {
+    constexpr int S = decltype(slot)::value;
+    commit(slot);
+    __syncthreads();
+    prefetch(slot, i0 + 16 * SQ_PF);
+    {
+      // delta of the tile: D[token][channel] = xdt[token][:] . dt_w[channel][:] (+ bias, softplus)
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[j * WP + 4 * s + g], wlw[4 * s + g], acc, 0, 0, 0);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = acc[r] + dtb;
+        v[r] = SOFTPLUS ? softplus_raw(x) : x;
+      }
+      *reinterpret_cast<float4*>(dlw + 4 * g) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) quad(q);
+    __syncthreads();
+    {
+      const int i = i0 + ut, l = pos_of(i);
+      const bool ok = i < Lend && dbase + uc < p.D && l < p.n_keep;
+      const uint2 v = *reinterpret_cast<const uint2*>(&ys[ut * SQ_UP + uc]);
+      __builtin_amdgcn_raw_buffer_store_b64((u32x2_t){v.x, v.y}, ry, (int)(ok ? (unsigned)(l * p.ldy + uc) * 2u : OOB),
+                                            0, 0);
+    }
+  };
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  prefetch(S0{}, 0);
+  if constexpr (SQ_PF == 2) {
+    prefetch(S1{}, 16);
+    for (int i0 = 0; i0 < Lend; i0 += 32) {   // an odd tile count runs one all-masked tile (loads 0, no stores)
+      tile(i0, S0{});
+      tile(i0 + 16, S1{});
+    }
+  } else {
+    for (int i0 = 0; i0 < Lend; i0 += 16) tile(i0, S0{});
+  }
+}
+
+template <int R>
+static int launch_scan_quad(const ActhScanDesc& a, const ActhScanDesc& b, int nb_total, hipStream_t stream) {
+  const int gx = (a.D + SQ_CH - 1) / SQ_CH;
+  const dim3 grid((unsigned)(gx * 2 * nb_total));
+  if (a.softplus) hipLaunchKernelGGL((scan_quad_kernel<R, true>), grid, dim3(SQ_NT), 0, stream, a, b, a.nb, gx);
+  else hipLaunchKernelGGL((scan_quad_kernel<R, false>), grid, dim3(SQ_NT), 0, stream, a, b, a.nb, gx);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
+static int dispatch_scan_quad(const ActhScanDesc& a, const ActhScanDesc& b, int nb_total, hipStream_t stream) {
+  switch (a.R) {
+    case 1: return launch_scan_quad<1>(a, b, nb_total, stream);
+    case 2: return launch_scan_quad<2>(a, b, nb_total, stream);
+    case 3: return launch_scan_quad<3>(a, b, nb_total, stream);
+    case 4: return launch_scan_quad<4>(a, b, nb_total, stream);
+    case 5: return launch_scan_quad<5>(a, b, nb_total, stream);
+    case 6: return launch_scan_quad<6>(a, b, nb_total, stream);
+    case 8: return launch_scan_quad<8>(a, b, nb_total, stream);
+    case 16: return launch_scan_quad<16>(a, b, nb_total, stream);
+    case 20: return launch_scan_quad<20>(a, b, nb_total, stream);
+    case 40: return launch_scan_quad<40>(a, b, nb_total, stream);
+    case 80: return launch_scan_quad<80>(a, b, nb_total, stream);
+    default: return ACTH_EINVAL;
+  }
+}
+
 template <int R>
 static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
   const unsigned gx = (d.D + SC_THREADS - 1) / SC_THREADS;
@@ -535,7 +783,18 @@ static int scan_prepare(ActhScanDesc& d) {
   if (d.R == 0 && !d.delta) return ACTH_EINVAL;
   if (d.N != 16 || d.R < 0 || d.L <= 0 || d.D <= 0 || d.nb <= 0) return ACTH_EINVAL;
   if (d.G < 1 || d.G > 65535 || (d.flip1 && d.G != 2) || (d.y1 && d.G != 2)) return ACTH_EINVAL;
-  if (d.n_keep < 0 || d.n_keep > d.L || d.ldx < d.G * (d.R + 32)) return ACTH_EINVAL;
+  if (d.n_keep < 0 || d.n_keep > d.L) return ACTH_EINVAL;
+  if (d.xdbl_bf16) {
+    // bf16 xdbl: the fused SS2D form only (scan_quad_kernel), rows of [dt (R4) | B | C] per direction
+    if (d.R <= 0 || d.G != 2 || !d.flip1 || d.u_gstride != 0 || d.nchunks > 1) return ACTH_EINVAL;
+    if (d.ldx < 2 * (((d.R + 3) & ~3) + 32) || d.ldx % 4 || d.ldy % 4) return ACTH_EINVAL;
+    // one batch element's u / xdbl / y rows must be addressable by a 32-bit buffer offset
+    if ((long long)d.L * d.ldu * 2 >= (1ll << 31) || (long long)d.L * d.ldx * 2 >= (1ll << 31) ||
+        (long long)d.n_keep * d.ldy * 2 >= (1ll << 31))
+      return ACTH_EINVAL;
+  } else if (d.ldx < d.G * (d.R + 32)) {
+    return ACTH_EINVAL;
+  }
   if (d.D % 8 || d.ldu % 8 || (d.delta && (d.D % 4 || d.ld_delta % 4))) return ACTH_EINVAL;
   if (d.n_keep == 0) return 1;
   if (d.nchunks < 1) d.nchunks = 1;
@@ -556,6 +815,7 @@ extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
   ActhScanDesc d = *dp;
   const int rc = scan_prepare(d);
   if (rc != ACTH_OK) return rc == 1 ? ACTH_OK : rc;
+  if (d.xdbl_bf16) return dispatch_scan_quad(d, d, d.nb, stream);
   switch (d.R) {
     case 0: return launch_scan<0>(d, stream);
     case 1: return launch_scan<1>(d, stream);
@@ -592,13 +852,14 @@ extern "C" int acth_selective_scan2(const ActhScanDesc* d0p, const ActhScanDesc*
   const int ra = scan_prepare(a), rb = scan_prepare(b);
   if ((ra != ACTH_OK && ra != 1) || (rb != ACTH_OK && rb != 1)) return ACTH_EINVAL;
   if (ra == 1 || rb == 1 || a.nchunks > 1 || b.nchunks > 1 || a.R != b.R || a.D != b.D || a.G != b.G ||
-      a.softplus != b.softplus || (long long)a.nb + b.nb > 65535) {
+      a.softplus != b.softplus || a.xdbl_bf16 != b.xdbl_bf16 || (long long)a.nb + b.nb > 65535) {
     // nothing to pair: the separate launches
     int rc = ACTH_OK;
     if (ra != 1) rc = acth_selective_scan(d0p, stream);
     if (rc == ACTH_OK && rb != 1) rc = acth_selective_scan(d1p, stream);
     return rc;
   }
+  if (a.xdbl_bf16) return dispatch_scan_quad(a, b, a.nb + b.nb, stream);
   switch (a.R) {
     case 0: return launch_scan2<0>(a, b, stream);
     case 1: return launch_scan2<1>(a, b, stream);

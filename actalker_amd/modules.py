@@ -663,8 +663,15 @@ class SS2D_Unit(nn.Module):
         c = self.__dict__.setdefault("_acth_cache", {})
         if "p" not in c:
             with torch.no_grad():
+                K, R, Din = self.num_direction, self.dt_rank, self.d_inner
+                R4 = (R + 3) // 4 * 4
+                xw = self.x_proj_weight.detach()
+                if R4 != R:      # [dt (R) | 0 (R4 - R) | B | C] per direction: 8-byte aligned bf16 rows
+                    pad = torch.zeros((K, R4 - R, Din), device=xw.device, dtype=xw.dtype)
+                    xw = torch.cat([xw[:, :R], pad, xw[:, R:]], dim=1)
                 c["p"] = dict(
                     xproj=_bf(self.x_proj_weight.reshape(-1, self.d_inner)),
+                    xproj_pad=_bf(xw.reshape(-1, Din)),
                     dt_w=_f32(self.dt_projs_weight),
                     dt_b=_f32(self.dt_projs_bias),
                     A_log=_f32(self.A_logs),
@@ -674,10 +681,17 @@ class SS2D_Unit(nn.Module):
     def _acth_invalidate(self):
         self.__dict__["_acth_cache"] = {}
 
+    # x_proj output rows in bf16 (the reference's x_dbl dtype, mamba_layer.py:1521) for scan_quad_kernel;
+    # False: fp32 rows and the paired-lane kernel (ACTH_SCAN_XDBL_F32=1)
+    acth_xdbl_bf16 = os.environ.get("ACTH_SCAN_XDBL_F32", "0") != "1"
+
     def scan_args(self, u, nb, L, n_keep):
         """x_proj of u (the GEMM ahead of the scan) and the scan's arguments."""
         p = self.packed()
-        xdbl = ops.gemm(u, p["xproj"], out_f32=True)
+        if self.acth_xdbl_bf16:
+            xdbl = ops.gemm(u, p["xproj_pad"])
+        else:
+            xdbl = ops.gemm(u, p["xproj"], out_f32=True)
         return dict(u=u, xdbl=xdbl, dt_w=p["dt_w"], dt_b=p["dt_b"], A_log=p["A_log"], Dskip=p["D"], nb=nb, L=L,
                     R=self.dt_rank, n_keep=n_keep)
 

@@ -494,7 +494,8 @@ def mamba_combine_ln(branch_a: dict, branch_e: dict, gamma, beta, eps: float, M:
 def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks):
     """Checks and ScanDesc of one fused bidirectional scan; (None, y0, y1, None) when n_keep is 0."""
     _need(u, torch.bfloat16, "scan u")
-    _need(xdbl, torch.float32, "scan xdbl")
+    if xdbl.dtype not in (torch.float32, torch.bfloat16):
+        raise _lib.ActhError(f"scan xdbl must be float32 or bfloat16, got {xdbl.dtype}")
     D = u.shape[1]
     for t, nm in ((dt_w, "dt_w"), (dt_b, "dt_b"), (A_log, "A_log"), (Dskip, "D")):
         _need(t, torch.float32, "scan " + nm)
@@ -513,13 +514,19 @@ def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1
     d.y0, d.y1, d.ldy = y0.data_ptr(), y1.data_ptr(), _rows(y0, "scan y0")
     d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, R, 16, n_keep
     d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = 1, 2, 0, 0, 1
+    d.xdbl_bf16 = int(xdbl.dtype == torch.bfloat16)
+    if d.xdbl_bf16:
+        d.nchunks = 1          # the bf16-xdbl kernel is single-pass
+        return d, y0, y1, None
     ws = _scan_chunking(d, nb, 2, D, L, nchunks, u.device)
     return d, y0, y1, ws
 
 
 def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip, *, nb: int, L: int, R: int,
                    n_keep: int, y0=None, y1=None, nchunks: Optional[int] = None):
-    """Fused bidirectional scan. u: (nb*L, D) bf16, xdbl: (nb*L, 2*(R+32)) fp32."""
+    """Fused bidirectional scan. u: (nb*L, D) bf16; xdbl: (nb*L, 2*(R+32)) fp32 rows [dt | B | C] per
+    direction, or bf16 rows (the reference's x_dbl dtype) of 2*(R4+32) with R4 = R rounded up to 4
+    (dt padding columns ignored; ``xproj_rows_padded`` packs x_proj weights to that layout)."""
     lib = _lib.load()
     d, y0, y1, ws = _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks)
     if d is not None:

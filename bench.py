@@ -207,7 +207,7 @@ class GemmTimer:
 class FamilyTimer:
     """HIP events around every launch of the non-GEMM kernel families on the launch stream inside the
     timed region, with each launch's algorithmic work: flash attention FLOPs (4 S^2 64 per head and
-    batch), fused level-0 feed-forward FLOPs (24 M C^2), selective-scan bytes (u read once for both directions, the fp32 xdbl rows, both outputs
+    batch), fused level-0 feed-forward FLOPs (24 M C^2), selective-scan bytes (u read once for both directions, the xdbl rows (bf16, or fp32 on the legacy path), both outputs
     written), GroupNorm / LayerNorm bytes (input read once, output written once -- the stats pass's
     second read of the input is the kernels' cost, not the algorithm's)."""
 
@@ -238,7 +238,7 @@ class FamilyTimer:
 
         def w_scan(u, xdbl, *a, nb, L, R, n_keep, **k):
             D = u.shape[1]
-            return nb * L * D * 2 + nb * L * xdbl.shape[1] * 4 + 2 * nb * n_keep * D * 2
+            return nb * L * D * 2 + nb * L * xdbl.shape[1] * xdbl.element_size() + 2 * nb * n_keep * D * 2
 
         def w_scan2(a, b):
             return sum(w_scan(**d) for d in (a, b))

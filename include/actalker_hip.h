@@ -219,6 +219,9 @@ typedef struct ActhScanDesc {
   int nchunks;                /* >1: two-pass chunked scan (needs ws); 0/1: single pass */
   int chunk_len;              /* derived by the library (ignored on input) */
   float* ws;                  /* acth_selective_scan_workspace_size(nb, G, D, nchunks) bytes */
+  int xdbl_bf16;              /* 1: xdbl rows are bf16 (the reference's x_dbl dtype, mamba_layer.py:1521),
+                                 per direction [dt (R rounded up to 4, padding ignored) | B(16) | C(16)];
+                                 fused SS2D form only (R > 0, G = 2, flip1, single pass) */
 } ActhScanDesc;
 int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream);
 /* Both SS2D branches of SS2D_cond_v10 (audio d0, expression d1; mamba_layer.py:1955-1986) in one

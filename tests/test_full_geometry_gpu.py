@@ -90,11 +90,14 @@ def _bf(t):
     return t.to(torch.bfloat16)
 
 
+@pytest.mark.parametrize("xdt", ["f32", "bf16"])
 @pytest.mark.parametrize("S,C,n_cond", [(9216, 320, 33), (9216, 320, 2), (2304, 640, 33), (576, 1280, 33)])
-def test_selective_scan_level_shapes(dev, S, C, n_cond):
+def test_selective_scan_level_shapes(dev, S, C, n_cond, xdt):
     """One batch element of a level's scan: L = S + n_cond (audio branch 33 = ID + 32 audio tokens,
     expression branch 2 = ID + 1 VASA token), D = d_inner = 2C, R = ceil(C / 16), outputs kept for
-    the S image tokens (mamba_layer.py:1965-1969, 1505-1548)."""
+    the S image tokens (mamba_layer.py:1965-1969, 1505-1548). xdt: the x_proj rows fed to the scan in
+    fp32 (paired-lane kernel) or bf16 (scan_quad_kernel; the reference's half-precision x_dbl,
+    mamba_layer.py:1521, which the oracle then also uses)."""
     from actalker_amd import ops
     g = torch.Generator().manual_seed(S + n_cond)
     D, R, L = 2 * C, -(-C // 16), S + n_cond
@@ -107,12 +110,16 @@ def test_selective_scan_level_shapes(dev, S, C, n_cond):
     alog = torch.log(torch.arange(1, 17).float()).repeat(2 * D, 1) + 0.1 * torch.randn(2 * D, 16, generator=g)
     Dp = 1 + 0.1 * torch.randn(2 * D, generator=g)
     xdbl = u.float() @ _bf(xproj).float().t()
+    if xdt == "bf16":
+        xdbl = _bf(xdbl)
     y0, y1 = ops.selective_scan(u.to(dev), xdbl.to(dev), dtw.to(dev), dtb.to(dev), alog.to(dev), Dp.to(dev),
                                 nb=1, L=L, R=R, n_keep=S)
     W = R + 32
     x = u.float().t()[None]                                        # (1, D, L)
     xs = torch.stack([x, torch.flip(x, dims=[-1])], 1)
     x_dbl = torch.einsum("b k d l, k c d -> b k c l", xs, _bf(xproj).float().view(2, W, D))
+    if xdt == "bf16":
+        x_dbl = _bf(x_dbl).float()
     dts, Bs, Cs = torch.split(x_dbl, [R, 16, 16], dim=2)
     dts = torch.einsum("b k r l, k d r -> b k d l", dts, dtw)
     out = ref.selective_scan_ref(xs.reshape(1, 2 * D, L), dts.reshape(1, 2 * D, L), -torch.exp(alog), Bs, Cs, Dp,
@@ -120,7 +127,7 @@ def test_selective_scan_level_shapes(dev, S, C, n_cond):
     r0 = out[0, 0, :, :S].t()
     r1 = torch.flip(out[0, 1], dims=[-1])[:, :S].t()
     s0, s1 = _stats(y0, r0), _stats(y1, r1)
-    _log(f"scan_L{L}_D{D}", dict(dir0=s0, dir1=s1))
+    _log(f"scan_L{L}_D{D}_{xdt}", dict(dir0=s0, dir1=s1))
     assert s0["rel_l2"] < 1e-2 and s1["rel_l2"] < 1e-2, (s0, s1)
 
 

@@ -660,18 +660,69 @@ def test_selective_scan_fused(dev, nb, L, D, R, n_keep, nchunks):
     assert rel(y1, r1) < 1e-2
 
 
+def _pad_xproj(xproj, R):
+    """x_proj rows [dt (R) | B | C] per direction -> [dt (R) | 0 (R4 - R) | B | C] (SS2D_Unit.packed)."""
+    W, D = R + 32, xproj.shape[1]
+    R4 = (R + 3) // 4 * 4
+    x = xproj.view(2, W, D)
+    return torch.cat([x[:, :R], torch.zeros(2, R4 - R, D), x[:, R:]], 1).reshape(-1, D)
+
+
+@pytest.mark.parametrize("nb,L,D,R,n_keep", [
+    (2, 40, 64, 4, 30), (1, 300, 640, 20, 267), (2, 97, 1280, 40, 64), (1, 33, 2560, 80, 0), (3, 17, 128, 80, 17),
+    (1, 1000, 128, 20, 968), (2, 50, 72, 5, 40), (3, 61, 200, 8, 61), (2, 23, 48, 1, 20), (1, 64, 256, 3, 5)])
+def test_selective_scan_quad(dev, nb, L, D, R, n_keep):
+    """bf16 x_proj rows (scan_quad_kernel): the reference's data flow with a half-precision x_dbl
+    (mamba_layer.py:1521) -- the oracle scans the same bf16-rounded rows; dt padding columns (R % 4)
+    must be ignored (filled with garbage here). Also == the paired-lane kernel fed those rows in fp32."""
+    g = torch.Generator().manual_seed(nb * 1000 + L + R)
+    u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
+    R4 = (R + 3) // 4 * 4
+    xpad = _pad_xproj(bf(xproj).float(), R)
+    xdbl = bf(u.float() @ xpad.t())                                 # (nb*L, 2*(R4+32)) bf16
+    if R4 != R:                                                     # padding columns are ignored
+        xv = xdbl.view(nb * L, 2, R4 + 32)
+        xv[:, :, R:R4] = bf(torch.full((nb * L, 2, R4 - R), 7.0))
+    args = dict(dt_w=dtw.to(dev), dt_b=dtb.to(dev), A_log=alog.to(dev), Dskip=Dp.to(dev), nb=nb, L=L, R=R,
+                n_keep=n_keep)
+    y0, y1 = ops.selective_scan(u.to(dev), xdbl.to(dev), **args)
+    if n_keep == 0:
+        return
+    W = R + 32
+    x = u.float().view(nb, L, D).permute(0, 2, 1)
+    xs = torch.stack([x, torch.flip(x, dims=[-1])], 1)
+    x_dbl = bf(torch.einsum("b k d l, k c d -> b k c l", xs, bf(xproj).float().view(2, W, D))).float()
+    dts, Bs, Cs = torch.split(x_dbl, [R, 16, 16], dim=2)
+    dts = torch.einsum("b k r l, k d r -> b k d l", dts, dtw)
+    out = ref.selective_scan_ref(xs.reshape(nb, 2 * D, L), dts.reshape(nb, 2 * D, L), -torch.exp(alog), Bs, Cs,
+                                 Dp, delta_bias=dtb.reshape(-1), delta_softplus=True).view(nb, 2, D, L)
+    r0 = out[:, 0, :, :n_keep].permute(0, 2, 1).reshape(-1, D)
+    r1 = torch.flip(out[:, 1], dims=[-1])[:, :, :n_keep].permute(0, 2, 1).reshape(-1, D)
+    assert rel(y0, r0) < 1e-2
+    assert rel(y1, r1) < 1e-2
+    # the same rows in fp32 through the paired-lane kernel (unpadded layout)
+    xf = xdbl.float().view(nb * L, 2, R4 + 32)
+    xf = torch.cat([xf[:, :, :R], xf[:, :, R4:]], 2).reshape(nb * L, 2 * W).contiguous()
+    p0, p1 = ops.selective_scan(u.to(dev), xf.to(dev), nchunks=1, **args)
+    assert rel(y0, p0) < 4e-3 and rel(y1, p1) < 4e-3
+
+
 @pytest.mark.parametrize("ca,cb", [
     ((2, 300, 640, 20, 267), (2, 45, 640, 20, 40)),        # same kernel config, different L / n_keep
     ((3, 97, 1280, 40, 64), (1, 33, 1280, 40, 33)),        # different nb
     ((2, 40, 64, 4, 30), (2, 40, 64, 8, 30)),              # different R: two launches
     ((2, 40, 64, 4, 0), (2, 50, 64, 4, 50))])              # one branch empty
-def test_selective_scan2_matches_single(dev, ca, cb):
+@pytest.mark.parametrize("xdt", ["f32", "bf16"])
+def test_selective_scan2_matches_single(dev, ca, cb, xdt):
     """acth_selective_scan2 (both SS2D branches in one launch) == two acth_selective_scan calls, bit for bit."""
     args, singles = [], []
     for i, (nb, L, D, R, n_keep) in enumerate((ca, cb)):
         g = torch.Generator().manual_seed(7 + i * 31 + L)
         u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
-        xdbl = u.float() @ bf(xproj).float().t()
+        if xdt == "bf16":
+            xdbl = bf(u.float() @ _pad_xproj(bf(xproj).float(), R).t())
+        else:
+            xdbl = u.float() @ bf(xproj).float().t()
         a = dict(u=u.to(dev), xdbl=xdbl.to(dev), dt_w=dtw.to(dev), dt_b=dtb.to(dev), A_log=alog.to(dev),
                  Dskip=Dp.to(dev), nb=nb, L=L, R=R, n_keep=n_keep)
         args.append(a)

@@ -15,33 +15,51 @@ from actalker_amd import ops  # noqa: E402
 SHAPES = [(84, 9249, 640, 20), (84, 2337, 1280, 40), (84, 609, 2560, 80)]   # the bench step: 6 units x 14 frames
 
 
-def main(iters=3):
+def main(iters=3, only_quad=False):
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
-    for nb, L, D, R in SHAPES:
+    shapes = SHAPES
+    if "--shape" in sys.argv:
+        shapes = [tuple(int(v) for v in a.split(",")) for a in sys.argv[sys.argv.index("--shape") + 1:]]
+    for nb, L, D, R in shapes:
         u = torch.randn(nb * L, D, generator=g).to(dev, torch.bfloat16)
         xdbl = (0.3 * torch.randn(nb * L, 2 * (R + 32), generator=g)).to(dev)
         dtw = (0.1 * torch.randn(2, D, R, generator=g)).to(dev)
         dtb = torch.full((2, D), -3.0).to(dev)
         alog = torch.log(torch.arange(1, 17).float()).repeat(2 * D, 1).to(dev)
         Dp = torch.ones(2 * D).to(dev)
-        n_keep = L - 33
+        n_keep = L - 33 if L > 33 else L
         res = {}
-        variants = [("pair", 1), ("chunk2", 2), ("chunk4", 4)]
-        for name, nc in variants:
+        xbf = xdbl.to(torch.bfloat16)
+        variants = [("pair", 1, xdbl), ("quad", 1, xbf), ("chunk2", 2, xdbl)]
+        if only_quad:
+            variants = [("quad", 1, xbf)]
+        for name, nc, xd in variants:
             args = dict(nb=nb, L=L, R=R, n_keep=n_keep, nchunks=nc)
-            y = ops.selective_scan(u, xdbl, dtw, dtb, alog, Dp, **args)
+            y = ops.selective_scan(u, xd, dtw, dtb, alog, Dp, **args)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(iters):
-                ops.selective_scan(u, xdbl, dtw, dtb, alog, Dp, **args)
+                ops.selective_scan(u, xd, dtw, dtb, alog, Dp, **args)
             e1.record()
             torch.cuda.synchronize()
             res[name] = (e0.elapsed_time(e1) / iters, y)
-        ref = res["pair"][1]
+        # mode 2: both branches (audio L, expression L - 31) in one paired launch
+        for name, xd in ((("quad2", xbf),) if only_quad else (("pair2", xdbl), ("quad2", xbf))):
+            La = dict(u=u, xdbl=xd, dt_w=dtw, dt_b=dtb, A_log=alog, Dskip=Dp, nb=nb, L=L, R=R, n_keep=n_keep)
+            ops.selective_scan2(La, dict(La))
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                ops.selective_scan2(La, dict(La))
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"  {name} (two branches, one launch) {e0.elapsed_time(e1) / iters:.3f} ms", flush=True)
+        ref = res[variants[0][0]][1]
         cells = []
-        for name, _ in variants:
+        for name, _, _ in variants:
             err = max(((res[name][1][i].float() - ref[i].float()).norm() / ref[i].float().norm()).item()
                       for i in range(2))
             cells.append(f"{name} {res[name][0]:.3f} ms (d {err:.1e})")
@@ -49,4 +67,4 @@ def main(iters=3):
 
 
 if __name__ == "__main__":
-    main()
+    main(only_quad="--quad" in sys.argv)

@@ -36,10 +36,12 @@ def main():
         for _ in range(a.iters):
             ops.flash_attn(qkv, nb, S, H)
         torch.cuda.synchronize()
-    elif a.kind == "scan":
+    elif a.kind in ("scan", "scanq"):          # scanq: bf16 x_proj rows (scan_quad_kernel)
         nb, L, D, R = a.args
         u = torch.randn(nb * L, D, generator=g).to(dev, torch.bfloat16)
         xdbl = (0.3 * torch.randn(nb * L, 2 * (R + 32), generator=g)).to(dev)
+        if a.kind == "scanq":
+            xdbl = xdbl.to(torch.bfloat16)
         dtw = (0.1 * torch.randn(2, D, R, generator=g)).to(dev)
         dtb = torch.full((2, D), -3.0).to(dev)
         alog = torch.log(torch.arange(1, 17).float()).repeat(2 * D, 1).to(dev)

@@ -165,7 +165,7 @@ class ScanDesc(ctypes.Structure):
         ("delta", c_vp), ("ld_delta", c_int), ("delta_f32", c_int), ("softplus", c_int),
         ("G", c_int), ("u_gstride", c_int), ("y_gstride", c_int), ("flip1", c_int),
         ("nchunks", c_int), ("chunk_len", c_int), ("ws", c_vp),
-        ("xdbl_bf16", c_int),
+        ("xdbl_bf16", c_int), ("scan_algo", c_int),
     ]
 
 

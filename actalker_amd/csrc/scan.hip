@@ -24,9 +24,12 @@
 // tile of SC_T tokens, read back as broadcasts; the next tile is prefetched into registers while
 // the current one is scanned. State and exp(A) constants stay in registers.
 #include "common.h"
+#include <type_traits>
 
 #define SC_T 16
 #define SC_THREADS 128
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -240,10 +243,22 @@ __device__ __forceinline__ float pair_swap(float v) {
 // repeat leave the serial loop.
 // Two descriptors: blocks with blockIdx.z < nb0 scan p0's batch elements, the rest p1's (the two SS2D
 // branches of one Mamba block in one launch, acth_selective_scan2); a single scan passes p1 = p0.
-template <int R, int CH, bool SOFTPLUS>
+// XB: xdbl rows in bf16 ([dt (R4) | B | C] per direction, the reference's x_dbl dtype), staged to fp32 in LDS;
+// the grid is then 1-D and dealt XCD-major (the channel blocks of one (batch, direction) share an L2), and the
+// forward direction stops at n_keep.
+template <int R, int CH, bool SOFTPLUS, bool XB = false>
 __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(const ActhScanDesc p0,
                                                                              const ActhScanDesc p1, int nb0) {
-  const bool second = (int)blockIdx.z >= nb0;
+  int bxi = blockIdx.x, kyi = blockIdx.y, bzi = blockIdx.z;
+  if constexpr (XB) {
+    const unsigned P = blockIdx.x, NB = gridDim.x, gx = (p0.D + CH - 1) / CH;
+    const unsigned xcd = P & 7, q8 = NB >> 3, r8 = NB & 7;
+    const unsigned wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (P >> 3);
+    bxi = (int)(wg % gx);
+    kyi = (int)((wg / gx) & 1);
+    bzi = (int)((wg / gx) >> 1);
+  }
+  const bool second = bzi >= nb0;
   const ActhScanDesc& p = *(second ? &p1 : &p0);  // wave-uniform: scalar loads from the kernarg segment
   constexpr int NT = 2 * CH;                     // threads
   constexpr int SP_CH = CH;
@@ -257,16 +272,18 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
   constexpr int DLP = SP_CH + 4;                 // delta tile row (padded: the 16 token rows of an
                                                  // accumulator store land in different banks)
   constexpr int NX = (SC_T * W + NT - 1) / NT;
+  constexpr int XQ = (R4 + 32) / 4;              // XB: 8-byte chunks of a bf16 token row
+  constexpr int NXB = (SC_T * XQ + NT - 1) / NT;
   static_assert(CH % 32 == 0, "a wave owns 32 channels");
   __shared__ __attribute__((aligned(16))) float xs[SC_T * WP];
   __shared__ __attribute__((aligned(16))) bf16_t us[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) bf16_t ys[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) float dls[SC_T * DLP];
 
-  const int k = blockIdx.y, b = (int)blockIdx.z - (second ? nb0 : 0);
+  const int k = kyi, b = bzi - (second ? nb0 : 0);
   const int t = threadIdx.x;
   const int half = t & 1, cl = t >> 1;           // state half, channel within the block
-  const int dbase = blockIdx.x * SP_CH;
+  const int dbase = bxi * SP_CH;
   const int d = dbase + cl;
   const bool active = d < p.D;
   const int dd = active ? d : 0;
@@ -310,27 +327,60 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
 
   const bf16_t* ub = (const bf16_t*)p.u + (size_t)b * p.L * p.ldu + (size_t)k * p.u_gstride + dbase;
   const float* xb = p.xdbl + (size_t)b * p.L * p.ldx + k * W;
+  const bf16_t* xbh = (const bf16_t*)p.xdbl + (size_t)b * p.L * p.ldx + k * (R4 + 32);
   const size_t dl_off = (size_t)b * p.L * p.ld_delta + (size_t)k * p.D + dbase;
   bf16_t* yb = (p.y1 && k == 1) ? (bf16_t*)p.y1 : (bf16_t*)p.y0 + (size_t)k * p.y_gstride;
   yb += (size_t)b * p.n_keep * p.ldy + dbase;
+  // XB: the forward direction stops at n_keep (later tokens only feed a state nobody reads)
+  const int Lend = (XB && !rev) ? p.n_keep : p.L;
 
   auto pos_of = [&](int i) { return rev ? p.L - 1 - i : i; };
-  float px[NX];
-  uint4 pu;
+  // XB: branch-free global traffic (buffer ops; masked lanes carry an out-of-range offset: loads return 0,
+  // stores are dropped) through a 2-tile register ring, so the compiler's s_waitcnt keeps the younger
+  // tile's loads and the previous tile's y stores in flight instead of draining to vmcnt(0) every tile
+  constexpr int NS = XB ? 2 : 1;
+  const unsigned OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(xbh), (short)0, (int)((size_t)p.L * p.ldx * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ru =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(ub), (short)0, (int)((size_t)p.L * p.ldu * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc(yb, (short)0, (int)((size_t)p.n_keep * p.ldy * 2), 0x00020000);
+  float px[XB ? 1 : NX];
+  uint2 pxh[NS][XB ? NXB : 1];
+  uint4 pu[NS];
   float4 pd[R == 0 ? 2 : 1];
-  auto prefetch = [&](int i0) {
+  auto prefetch = [&](auto slot, int i0) {
+    constexpr int S = decltype(slot)::value;
+    if constexpr (XB) {
 #pragma unroll
-    for (int e = 0; e < NX; ++e) {
-      const int idx = t + e * NT;
-      const int tt = idx / W, col = idx - tt * W;
-      const int i = i0 + tt;
-      px[e] = (tt < SC_T && i < p.L) ? xb[(size_t)pos_of(i) * p.ldx + col] : 0.0f;
+      for (int e = 0; e < NXB; ++e) {
+        const int idx = t + e * NT, tt = idx / XQ, c4 = (idx - tt * XQ) * 4;
+        const bool ok = tt < SC_T && i0 + tt < Lend;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+            rx, (int)(ok ? (unsigned)(pos_of(i0 + tt) * p.ldx + c4) * 2u : OOB), 0, 0);
+        pxh[S][e] = make_uint2(v[0], v[1]);
+      }
+      const int tt = t / U16, cc = (t % U16) * 8;
+      const bool ok = i0 + tt < Lend && dbase + cc < p.D;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+          ru, (int)(ok ? (unsigned)(pos_of(i0 + tt) * p.ldu + cc) * 2u : OOB), 0, 0);
+      pu[S] = make_uint4(v[0], v[1], v[2], v[3]);
+      return;
+    } else {
+#pragma unroll
+      for (int e = 0; e < NX; ++e) {
+        const int idx = t + e * NT;
+        const int tt = idx / W, col = idx - tt * W;
+        const int i = i0 + tt;
+        px[e] = (tt < SC_T && i < p.L) ? xb[(size_t)pos_of(i) * p.ldx + col] : 0.0f;
+      }
     }
     {
       const int tt = t / U16, cc = (t % U16) * 8;   // NT x 16 B = 16 tokens x CH channels
       const int i = i0 + tt;
-      pu = (i < p.L && dbase + cc < p.D) ? *reinterpret_cast<const uint4*>(ub + (size_t)pos_of(i) * p.ldu + cc)
-                                         : make_uint4(0, 0, 0, 0);
+      pu[S] = (i < Lend && dbase + cc < p.D) ? *reinterpret_cast<const uint4*>(ub + (size_t)pos_of(i) * p.ldu + cc)
+                                             : make_uint4(0, 0, 0, 0);
     }
     if constexpr (R == 0) {
 #pragma unroll
@@ -353,16 +403,35 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
       }
     }
   };
-  auto commit = [&]() {
+  auto commit = [&](auto slot) {
+    constexpr int S = decltype(slot)::value;
+    if constexpr (XB) {
 #pragma unroll
-    for (int e = 0; e < NX; ++e) {
-      const int idx = t + e * NT;
-      if (idx < SC_T * W) {
-        const int tt = idx / W, col = idx - tt * W;
-        xs[tt * WP + (col < R ? col : col - R + R4)] = px[e];
+      for (int e = 0; e < NXB; ++e) {
+        const int idx = t + e * NT, tt = idx / XQ, c4 = (idx - tt * XQ) * 4;
+        if (tt < SC_T) {
+          const uint2 q = pxh[S][e];
+          float4 v = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                                 __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+          if (R4 > R && c4 + 4 == R4) {          // dt padding columns are ignored: zero (they meet zero weights)
+            if (R4 - R >= 1) v.w = 0.f;
+            if (R4 - R >= 2) v.z = 0.f;
+            if (R4 - R >= 3) v.y = 0.f;
+          }
+          *reinterpret_cast<float4*>(&xs[tt * WP + c4]) = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < NX; ++e) {
+        const int idx = t + e * NT;
+        if (idx < SC_T * W) {
+          const int tt = idx / W, col = idx - tt * W;
+          xs[tt * WP + (col < R ? col : col - R + R4)] = px[e];
+        }
       }
     }
-    *reinterpret_cast<uint4*>(&us[(t / U16) * SP_CH + (t % U16) * 8]) = pu;
+    *reinterpret_cast<uint4*>(&us[(t / U16) * SP_CH + (t % U16) * 8]) = pu[S];
     if constexpr (R == 0) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -407,13 +476,15 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
     }
   };
 
-  prefetch(0);
-  for (int i0 = 0; i0 < p.L; i0 += SC_T) {
-    commit();
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  auto tile = [&](int i0, auto slot) {
+    commit(slot);
     __syncthreads();
-    if (i0 + SC_T < p.L) prefetch(i0 + SC_T);
+    if constexpr (XB) prefetch(slot, i0 + 2 * SC_T);        // unconditional: past Lend every lane is masked
+    else if (i0 + SC_T < Lend) prefetch(slot, i0 + SC_T);
     delta_tile();
-    const int nt = min(SC_T, p.L - i0);
+    const int nt = max(0, min(SC_T, Lend - i0));
     // one token of the recurrence (partial last tile)
     auto token = [&](int tt) {
       const float* xr = xs + tt * WP;
@@ -489,13 +560,29 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
     {
       const int tt = t / U16, cc = (t % U16) * 8;
       const int i = i0 + tt;
-      if (tt < nt && dbase + cc < p.D) {
+      if constexpr (XB) {
+        const int l = pos_of(i);
+        const bool ok = tt < nt && dbase + cc < p.D && l < p.n_keep;
+        const uint4 v = *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){v.x, v.y, v.z, v.w}, ry,
+                                               (int)(ok ? (unsigned)(l * p.ldy + cc) * 2u : OOB), 0, 0);
+      } else if (tt < nt && dbase + cc < p.D) {
         const int l = pos_of(i);
         if (l < p.n_keep)
           *reinterpret_cast<uint4*>(yb + (size_t)l * p.ldy + cc) =
               *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
       }
     }
+  };
+  prefetch(S0{}, 0);
+  if constexpr (XB) {
+    prefetch(S1{}, SC_T);
+    for (int i0 = 0; i0 < Lend; i0 += 2 * SC_T) {   // an odd tile count runs one all-masked tile
+      tile(i0, S0{});
+      tile(i0 + SC_T, S1{});
+    }
+  } else {
+    for (int i0 = 0; i0 < Lend; i0 += SC_T) tile(i0, S0{});
   }
 }
 
@@ -542,7 +629,7 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
 #else
 #define SQ_TOKEN_FENCE() do {} while (0)
 #endif
-typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+
 #define SQ_UP (SQ_CH + 16)    // u / y tile row in bf16: 4 token rows land on disjoint banks
 
 template <int R, bool SOFTPLUS>
@@ -747,6 +834,33 @@ static int dispatch_scan_quad(const ActhScanDesc& a, const ActhScanDesc& b, int 
   }
 }
 
+// the paired-lane kernel on bf16 xdbl rows: 1-D grid dealt XCD-major inside the kernel
+template <int R>
+static int launch_pair_bf16(const ActhScanDesc& a, const ActhScanDesc& b, int nb_total, hipStream_t stream) {
+  const dim3 grid((unsigned)(((a.D + 127) / 128) * 2 * nb_total));
+  if (a.softplus) hipLaunchKernelGGL((scan_pair_kernel<R, 128, true, true>), grid, dim3(256), 0, stream, a, b, a.nb);
+  else hipLaunchKernelGGL((scan_pair_kernel<R, 128, false, true>), grid, dim3(256), 0, stream, a, b, a.nb);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
+static int dispatch_pair_bf16(const ActhScanDesc& a, const ActhScanDesc& b, int nb_total, hipStream_t stream) {
+  switch (a.R) {
+    case 1: return launch_pair_bf16<1>(a, b, nb_total, stream);
+    case 2: return launch_pair_bf16<2>(a, b, nb_total, stream);
+    case 3: return launch_pair_bf16<3>(a, b, nb_total, stream);
+    case 4: return launch_pair_bf16<4>(a, b, nb_total, stream);
+    case 5: return launch_pair_bf16<5>(a, b, nb_total, stream);
+    case 6: return launch_pair_bf16<6>(a, b, nb_total, stream);
+    case 8: return launch_pair_bf16<8>(a, b, nb_total, stream);
+    case 16: return launch_pair_bf16<16>(a, b, nb_total, stream);
+    case 20: return launch_pair_bf16<20>(a, b, nb_total, stream);
+    case 40: return launch_pair_bf16<40>(a, b, nb_total, stream);
+    case 80: return launch_pair_bf16<80>(a, b, nb_total, stream);
+    default: return ACTH_EINVAL;
+  }
+}
+
 template <int R>
 static int launch_scan(const ActhScanDesc& d, hipStream_t stream) {
   const unsigned gx = (d.D + SC_THREADS - 1) / SC_THREADS;
@@ -815,7 +929,7 @@ extern "C" int acth_selective_scan(const ActhScanDesc* dp, hipStream_t stream) {
   ActhScanDesc d = *dp;
   const int rc = scan_prepare(d);
   if (rc != ACTH_OK) return rc == 1 ? ACTH_OK : rc;
-  if (d.xdbl_bf16) return dispatch_scan_quad(d, d, d.nb, stream);
+  if (d.xdbl_bf16) return d.scan_algo == 1 ? dispatch_scan_quad(d, d, d.nb, stream) : dispatch_pair_bf16(d, d, d.nb, stream);
   switch (d.R) {
     case 0: return launch_scan<0>(d, stream);
     case 1: return launch_scan<1>(d, stream);
@@ -852,14 +966,16 @@ extern "C" int acth_selective_scan2(const ActhScanDesc* d0p, const ActhScanDesc*
   const int ra = scan_prepare(a), rb = scan_prepare(b);
   if ((ra != ACTH_OK && ra != 1) || (rb != ACTH_OK && rb != 1)) return ACTH_EINVAL;
   if (ra == 1 || rb == 1 || a.nchunks > 1 || b.nchunks > 1 || a.R != b.R || a.D != b.D || a.G != b.G ||
-      a.softplus != b.softplus || a.xdbl_bf16 != b.xdbl_bf16 || (long long)a.nb + b.nb > 65535) {
+      a.softplus != b.softplus || a.xdbl_bf16 != b.xdbl_bf16 || a.scan_algo != b.scan_algo ||
+      (long long)a.nb + b.nb > 65535) {
     // nothing to pair: the separate launches
     int rc = ACTH_OK;
     if (ra != 1) rc = acth_selective_scan(d0p, stream);
     if (rc == ACTH_OK && rb != 1) rc = acth_selective_scan(d1p, stream);
     return rc;
   }
-  if (a.xdbl_bf16) return dispatch_scan_quad(a, b, a.nb + b.nb, stream);
+  if (a.xdbl_bf16)
+    return a.scan_algo == 1 ? dispatch_scan_quad(a, b, a.nb + b.nb, stream) : dispatch_pair_bf16(a, b, a.nb + b.nb, stream);
   switch (a.R) {
     case 0: return launch_scan2<0>(a, b, stream);
     case 1: return launch_scan2<1>(a, b, stream);

@@ -7,6 +7,7 @@ allocator (device memory is torch's; compute is ours) and launches on
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import Optional, Sequence
 
@@ -491,6 +492,10 @@ def mamba_combine_ln(branch_a: dict, branch_e: dict, gamma, beta, eps: float, M:
     return out
 
 
+# bf16 x_proj rows: 0 = paired-lane kernel, 1 = scan_quad_kernel (MFMA input term; ACTH_SCAN_QUAD=1)
+SCAN_ALGO = int(os.environ.get("ACTH_SCAN_QUAD", "0"))
+
+
 def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks):
     """Checks and ScanDesc of one fused bidirectional scan; (None, y0, y1, None) when n_keep is 0."""
     _need(u, torch.bfloat16, "scan u")
@@ -515,6 +520,7 @@ def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1
     d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, R, 16, n_keep
     d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = 1, 2, 0, 0, 1
     d.xdbl_bf16 = int(xdbl.dtype == torch.bfloat16)
+    d.scan_algo = SCAN_ALGO
     if d.xdbl_bf16:
         d.nchunks = 1          # the bf16-xdbl kernel is single-pass
         return d, y0, y1, None

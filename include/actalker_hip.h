@@ -222,6 +222,7 @@ typedef struct ActhScanDesc {
   int xdbl_bf16;              /* 1: xdbl rows are bf16 (the reference's x_dbl dtype, mamba_layer.py:1521),
                                  per direction [dt (R rounded up to 4, padding ignored) | B(16) | C(16)];
                                  fused SS2D form only (R > 0, G = 2, flip1, single pass) */
+  int scan_algo;              /* bf16 xdbl: 0 paired-lane kernel (default), 1 scan_quad_kernel */
 } ActhScanDesc;
 int acth_selective_scan(const ActhScanDesc* d, hipStream_t stream);
 /* Both SS2D branches of SS2D_cond_v10 (audio d0, expression d1; mamba_layer.py:1955-1986) in one

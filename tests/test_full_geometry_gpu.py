@@ -90,15 +90,16 @@ def _bf(t):
     return t.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("xdt", ["f32", "bf16"])
+@pytest.mark.parametrize("xdt", ["f32", "bf16", "bf16q"])
 @pytest.mark.parametrize("S,C,n_cond", [(9216, 320, 33), (9216, 320, 2), (2304, 640, 33), (576, 1280, 33)])
-def test_selective_scan_level_shapes(dev, S, C, n_cond, xdt):
+def test_selective_scan_level_shapes(dev, S, C, n_cond, xdt, monkeypatch):
     """One batch element of a level's scan: L = S + n_cond (audio branch 33 = ID + 32 audio tokens,
     expression branch 2 = ID + 1 VASA token), D = d_inner = 2C, R = ceil(C / 16), outputs kept for
     the S image tokens (mamba_layer.py:1965-1969, 1505-1548). xdt: the x_proj rows fed to the scan in
     fp32 (paired-lane kernel) or bf16 (scan_quad_kernel; the reference's half-precision x_dbl,
     mamba_layer.py:1521, which the oracle then also uses)."""
     from actalker_amd import ops
+    monkeypatch.setattr(ops, "SCAN_ALGO", 1 if xdt == "bf16q" else 0)
     g = torch.Generator().manual_seed(S + n_cond)
     D, R, L = 2 * C, -(-C // 16), S + n_cond
     u = _bf(torch.randn(L, D, generator=g))
@@ -110,7 +111,7 @@ def test_selective_scan_level_shapes(dev, S, C, n_cond, xdt):
     alog = torch.log(torch.arange(1, 17).float()).repeat(2 * D, 1) + 0.1 * torch.randn(2 * D, 16, generator=g)
     Dp = 1 + 0.1 * torch.randn(2 * D, generator=g)
     xdbl = u.float() @ _bf(xproj).float().t()
-    if xdt == "bf16":
+    if xdt != "f32":
         xdbl = _bf(xdbl)
     y0, y1 = ops.selective_scan(u.to(dev), xdbl.to(dev), dtw.to(dev), dtb.to(dev), alog.to(dev), Dp.to(dev),
                                 nb=1, L=L, R=R, n_keep=S)
@@ -118,7 +119,7 @@ def test_selective_scan_level_shapes(dev, S, C, n_cond, xdt):
     x = u.float().t()[None]                                        # (1, D, L)
     xs = torch.stack([x, torch.flip(x, dims=[-1])], 1)
     x_dbl = torch.einsum("b k d l, k c d -> b k c l", xs, _bf(xproj).float().view(2, W, D))
-    if xdt == "bf16":
+    if xdt != "f32":
         x_dbl = _bf(x_dbl).float()
     dts, Bs, Cs = torch.split(x_dbl, [R, 16, 16], dim=2)
     dts = torch.einsum("b k r l, k d r -> b k d l", dts, dtw)

@@ -671,10 +671,13 @@ def _pad_xproj(xproj, R):
 @pytest.mark.parametrize("nb,L,D,R,n_keep", [
     (2, 40, 64, 4, 30), (1, 300, 640, 20, 267), (2, 97, 1280, 40, 64), (1, 33, 2560, 80, 0), (3, 17, 128, 80, 17),
     (1, 1000, 128, 20, 968), (2, 50, 72, 5, 40), (3, 61, 200, 8, 61), (2, 23, 48, 1, 20), (1, 64, 256, 3, 5)])
-def test_selective_scan_quad(dev, nb, L, D, R, n_keep):
-    """bf16 x_proj rows (scan_quad_kernel): the reference's data flow with a half-precision x_dbl
-    (mamba_layer.py:1521) -- the oracle scans the same bf16-rounded rows; dt padding columns (R % 4)
-    must be ignored (filled with garbage here). Also == the paired-lane kernel fed those rows in fp32."""
+@pytest.mark.parametrize("algo", [0, 1])
+def test_selective_scan_quad(dev, nb, L, D, R, n_keep, algo, monkeypatch):
+    """bf16 x_proj rows (algo 0: paired-lane kernel, 1: scan_quad_kernel): the reference's data flow with a
+    half-precision x_dbl (mamba_layer.py:1521) -- the oracle scans the same bf16-rounded rows; dt padding
+    columns (R % 4) must be ignored (filled with garbage here). Also == the paired-lane kernel fed those rows
+    in fp32."""
+    monkeypatch.setattr(ops, "SCAN_ALGO", algo)
     g = torch.Generator().manual_seed(nb * 1000 + L + R)
     u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
     R4 = (R + 3) // 4 * 4
@@ -712,14 +715,15 @@ def test_selective_scan_quad(dev, nb, L, D, R, n_keep):
     ((3, 97, 1280, 40, 64), (1, 33, 1280, 40, 33)),        # different nb
     ((2, 40, 64, 4, 30), (2, 40, 64, 8, 30)),              # different R: two launches
     ((2, 40, 64, 4, 0), (2, 50, 64, 4, 50))])              # one branch empty
-@pytest.mark.parametrize("xdt", ["f32", "bf16"])
-def test_selective_scan2_matches_single(dev, ca, cb, xdt):
+@pytest.mark.parametrize("xdt", ["f32", "bf16", "bf16q"])
+def test_selective_scan2_matches_single(dev, ca, cb, xdt, monkeypatch):
     """acth_selective_scan2 (both SS2D branches in one launch) == two acth_selective_scan calls, bit for bit."""
+    monkeypatch.setattr(ops, "SCAN_ALGO", 1 if xdt == "bf16q" else 0)
     args, singles = [], []
     for i, (nb, L, D, R, n_keep) in enumerate((ca, cb)):
         g = torch.Generator().manual_seed(7 + i * 31 + L)
         u, xproj, dtw, dtb, alog, Dp = _scan_case(nb, L, D, R, n_keep, g)
-        if xdt == "bf16":
+        if xdt != "f32":
             xdbl = bf(u.float() @ _pad_xproj(bf(xproj).float(), R).t())
         else:
             xdbl = u.float() @ bf(xproj).float().t()

@@ -31,10 +31,11 @@ def main(iters=3, only_quad=False):
         n_keep = L - 33 if L > 33 else L
         res = {}
         xbf = xdbl.to(torch.bfloat16)
-        variants = [("pair", 1, xdbl), ("quad", 1, xbf), ("chunk2", 2, xdbl)]
+        variants = [("pair", 1, xdbl), ("pairbf", 1, xbf), ("quad", 1, xbf)]
         if only_quad:
             variants = [("quad", 1, xbf)]
         for name, nc, xd in variants:
+            ops.SCAN_ALGO = 1 if name == "quad" else 0
             args = dict(nb=nb, L=L, R=R, n_keep=n_keep, nchunks=nc)
             y = ops.selective_scan(u, xd, dtw, dtb, alog, Dp, **args)
             torch.cuda.synchronize()
@@ -46,7 +47,8 @@ def main(iters=3, only_quad=False):
             torch.cuda.synchronize()
             res[name] = (e0.elapsed_time(e1) / iters, y)
         # mode 2: both branches (audio L, expression L - 31) in one paired launch
-        for name, xd in ((("quad2", xbf),) if only_quad else (("pair2", xdbl), ("quad2", xbf))):
+        for name, xd in ((("quad2", xbf),) if only_quad else (("pair2", xdbl), ("pairbf2", xbf), ("quad2", xbf))):
+            ops.SCAN_ALGO = 1 if name == "quad2" else 0
             La = dict(u=u, xdbl=xd, dt_w=dtw, dt_b=dtb, A_log=alog, Dskip=Dp, nb=nb, L=L, R=R, n_keep=n_keep)
             ops.selective_scan2(La, dict(La))
             torch.cuda.synchronize()

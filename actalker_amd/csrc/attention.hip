@@ -30,6 +30,19 @@ typedef __attribute__((address_space(3))) void lds_void;
 //  * P never leaves registers: S^T's accumulator rows are the B operand of the P.V product.
 
 #define FA_TILE 8192            // 64 keys x 128 B
+#ifndef FA_PRIO
+#define FA_PRIO 0
+#endif
+#ifndef FA_LATE_DMA
+#define FA_LATE_DMA 0
+#endif
+#if FA_PRIO
+#define FA_PRIO_ON() __builtin_amdgcn_s_setprio(1)
+#define FA_PRIO_OFF() __builtin_amdgcn_s_setprio(0)
+#else
+#define FA_PRIO_ON() do {} while (0)
+#define FA_PRIO_OFF() do {} while (0)
+#endif
 
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4_t lds_short4;
@@ -144,7 +157,7 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
   __builtin_amdgcn_s_barrier();
   int buf = 0;
   for (int kv0 = 0; kv0 < p.Skv; kv0 += 64) {
-    if (kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
+    if (!FA_LATE_DMA && kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
     const char* kt = smem + buf * 2 * FA_TILE;
     const char* vt = kt + FA_TILE;
 
@@ -159,11 +172,14 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
       for (int s = 0; s < 4; ++s) kf[sub][s] = *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4));
     }
     f32x16_t st[2];
+    FA_PRIO_ON();
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         st[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[sub][s], qf[s], s == 0 ? negm : st[sub], 0, 0, 0);
+    FA_PRIO_OFF();
+    if (FA_LATE_DMA && kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
     if (kv0 + 64 > p.Skv) {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -208,6 +224,7 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
         pf[sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
       }
     // ---- O^T += V^T P^T: A operand (d rows x 16 keys) by transpose reads of row-major V ----
+    FA_PRIO_ON();
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
@@ -234,6 +251,7 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
           else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[sub][s2], o1, 0, 0, 0);
         }
       }
+    FA_PRIO_OFF();
     // next tile landed (this wave's DMAs) and every wave is done reading `buf`
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

@@ -13,10 +13,10 @@ from actalker_amd import ops  # noqa: E402
 SHAPES = [(84, 9216, 5), (84, 2304, 10), (84, 576, 20), (84, 144, 20)]   # (frames, tokens, heads): the bench step
 
 
-def main(iters=5):
+def main(iters=5, flash_only=False):
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(0)
-    for nb, S, H in SHAPES:
+    for nb, S, H in (SHAPES[:2] if flash_only else SHAPES):
         qkv = torch.randn(nb * S, 3 * H * 64, generator=g).to(dev, torch.bfloat16)
         ops.flash_attn(qkv, nb, S, H)
         torch.cuda.synchronize()
@@ -29,6 +29,8 @@ def main(iters=5):
         ms = e0.elapsed_time(e1) / iters
         flops = 4.0 * nb * H * S * S * 64
         print(f"flash_attn nb={nb} S={S} H={H}: {ms:.3f} ms  {flops / ms / 1e9:.1f} TFLOP/s", flush=True)
+    if flash_only:
+        return
     # temporal attention over the 14 frames of a window (B = 4 CFG branches), HBM-bound
     for S, H in ((9216, 5), (2304, 10), (576, 20)):
         B, F = 4, 14
@@ -47,4 +49,4 @@ def main(iters=5):
 
 
 if __name__ == "__main__":
-    main()
+    main(flash_only="--flash" in sys.argv)

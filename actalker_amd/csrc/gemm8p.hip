@@ -88,7 +88,11 @@ __device__ unsigned long long g_gemm_stamps[STAMP_WGS * 4];
 // BN_ = 256: waves 2 (rows) x 4 (cols), a wave's quadrant share is 64 x 32 (4 x 2 fragments);
 // BN_ = 320 (the C = 320 projections and convs, one tile spans N): waves 4 x 2, share 32 x 80
 // (2 x 5 fragments), B half-tiles of 160 rows (20 DMA pieces: waves 0-3 issue 3, waves 4-7 two).
-template <int BN_, int AMODE>
+// TR: the MFMAs compute the transposed product (B fragment as the A operand), so a lane's accumulator holds
+// four consecutive columns of one row (used by the GEGLU launches, whose gated outputs then leave straight from
+// registers); TR = false keeps four consecutive rows of one column, which the slab-based epilogues write out
+// marginally faster (the convs measured 2-5 % slower transposed, profiles/r3_step24_*).
+template <int BN_, int AMODE, bool TR = false>
 __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, unsigned a_bytes, unsigned a2_bytes,
                                                         unsigned b_bytes, int vec_ok) {
   constexpr int WR = BN_ == 256 ? 2 : 4, WC = 8 / WR;
@@ -270,7 +274,8 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       for (int i = 0; i < TMQ; ++i)
 #pragma unroll
         for (int j = 0; j < TNQ; ++j)
-          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
+          c[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], c[i][j], 0, 0, 0)
+                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -365,15 +370,65 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   static_assert(8 * SR * EPI_LD * 4 <= 2 * BUF, "epilogue slabs");
   float* et = reinterpret_cast<float*>(smem) + wave * (SR * EPI_LD);
   const bool geglu = p.act == 2;
+  // c[i][j][r] = C[row 16 i + 4 fq + r][col 16 j + fr] (TR: C[row 16 i + fr][col 16 j + 4 fq + r], four
+  // consecutive columns: one ds_write_b128)
   auto slab = [&](const f32x4_t (&c)[TMQ][TNQ]) {
 #pragma unroll
     for (int i = 0; i < TMQ; ++i)
 #pragma unroll
-      for (int j = 0; j < TNQ; ++j)
+      for (int j = 0; j < TNQ; ++j) {
+        if constexpr (TR) {
+          *reinterpret_cast<f32x4_t*>(&et[(i * 16 + fr) * EPI_LD + j * 16 + 4 * fq]) = c[i][j];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) et[(i * 16 + fq * 4 + r) * EPI_LD + j * 16 + fr] = c[i][j][r];
+          for (int r = 0; r < 4; ++r) et[(i * 16 + fq * 4 + r) * EPI_LD + j * 16 + fr] = c[i][j][r];
+        }
+      }
   };
-  if (geglu) {
+  // GEGLU straight from the accumulators (BN_ = 256: a wave's 32 columns are one (hidden 16 | gate 16) granule
+  // pair, so c[i][0][r] and c[i][1][r] are the hidden and gate values of the same output column 4 fq + r): the
+  // gated outputs of fragment rows 2p and 2p + 1 are widened to 8 columns per lane by v_permlane16_swap (as the
+  // fast epilogue) and stored 16 bytes at a time; no LDS slab.
+  const bool geglu_direct = TR && geglu && BN_ == 256 && !p.out_f32 && p.orow_div >= p.M && vec_ok && !p.rmap &&
+                            (p.N & 31) == 0;
+  if (geglu_direct) {
+    if constexpr (TR && BN_ == 256) {
+      const int gl = fq & 1, gh = fq >> 1;
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        const int qm = qi >> 1, qn = qi & 1;
+        const f32x4_t (&c)[TMQ][TNQ] = acc[qm][qn];
+        const int lc0 = qn * (BN_ / 2) + wc * SC;
+        const float4 bh = *reinterpret_cast<const float4*>(&sbias[lc0 + 4 * fq]);
+        const float4 bg = *reinterpret_cast<const float4*>(&sbias[lc0 + 16 + 4 * fq]);
+        const float bhv[4] = {bh.x, bh.y, bh.z, bh.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+        const int ocol = (tile_n + lc0) / 2 + 8 * gh;
+#pragma unroll
+        for (int pp = 0; pp < TMQ / 2; ++pp) {
+          float o[2][4];
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+              const float2_pk gg = GEGLU_GELU((float2_pk){fmaf(c[2 * pp + h2][1][r], p.alpha, bgv[r]),
+                                                          fmaf(c[2 * pp + h2][1][r + 1], p.alpha, bgv[r + 1])});
+              o[h2][r] = fmaf(c[2 * pp + h2][0][r], p.alpha, bhv[r]) * gg.x;
+              o[h2][r + 1] = fmaf(c[2 * pp + h2][0][r + 1], p.alpha, bhv[r + 1]) * gg.y;
+            }
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(o[0][r]), __float_as_uint(o[1][r]), false, false);
+            v[r] = __uint_as_float(sw[0]);
+            v[4 + r] = __uint_as_float(sw[1]);
+          }
+          const int row = tile_m + qm * 128 + wr * SR + 16 * (2 * pp + gl) + fr;
+          if (row < p.M && ocol < p.N / 2)
+            *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)(row + p.orow_off) * p.ldc + ocol) = pack8(v);
+        }
+      }
+    }
+  } else if (geglu) {
     // BN_ = 256: one (hidden 16 | gate 16) granule pair -> 16 outputs: SR rows x 2 chunks per quadrant
     constexpr int NCH = SR * 2 / 64;
     static_assert(SR * 2 % 64 == 0, "GEGLU chunks per lane");
@@ -456,7 +511,10 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     };
     // Fast path for the UNet's residual-stream / conv epilogues (no activation, bf16 out, identity row
     // map, 16-byte aligned rows, whole 8-column chunks, residual without a row map, row bias staged in
-    // LDS): the combination of bias / row bias / residual / mix is a compile-time choice, so the chunk
+    // LDS; the slab transposes the accumulators so one store instruction writes whole 128-byte row
+    // segments: a register-direct variant, widened to 16 B per lane by v_permlane16_swap like the GEGLU path
+    // above, wrote 32-byte row pieces per instruction and measured 9-12 % slower on the K = 320 shapes,
+    // profiles/r3_step24_bench_gemm_epilogue_variants.log): the combination of bias / row bias / residual / mix is a compile-time choice, so the chunk
     // loop is branch-free, and each lane keeps one 8-column chunk across the quadrant's rows (its bias
     // chunk in registers, row-strided pointers) instead of re-deriving 64-bit addresses per chunk.
     // Measured with tools/gemm_stamps.py: the generic loop spent ~29k cycles per 256x320 tile.
@@ -585,6 +643,13 @@ extern "C" int acth_debug_gemm_stamps(unsigned long long* host_dst, int n_wgs) {
 template <int BN_>
 static void launch8p(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
                      int vec_ok, hipStream_t stream) {
+  if constexpr (BN_ == 256) {
+    if (d->act == 2 && d->amode == 0) {     // GEGLU: gated outputs straight from the transposed accumulators
+      hipLaunchKernelGGL((gemm8p_kernel<256, 0, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes,
+                         vec_ok);
+      return;
+    }
+  }
   if (d->amode == 1)
     hipLaunchKernelGGL((gemm8p_kernel<BN_, 1>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
   else if (d->amode == 2)

@@ -80,6 +80,14 @@ __device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, const RowPk& ri
 #define STAMP_WGS 16384
 __device__ unsigned long long g_gemm_stamps[STAMP_WGS * 4];
 
+#ifndef G8_TR_ALL
+#define G8_TR_ALL 0           // 0: transposed product for the GEGLU launches only; 1: every launch, with the TR fast
+                              // epilogue; 2: the launches without a residual / mix operand. Measured (same box,
+                              // profiles/r3_step26_*): 1 loses 7-10 % on residual GEMMs (8-byte fragment loads of the
+                              // residual) and +1 % per step; 2 gains 3-8 % on residual-free K = 320 shapes in
+                              // isolation but is within noise per step (360.3-361.0 vs 360.3-360.6 ms)
+#endif
+
 #define BAR() do { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); \
                    __builtin_amdgcn_sched_barrier(0); } while (0)
 
@@ -603,9 +611,105 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
         one(QM[qi], QN[qi], rbuf[qi % NRB], mbuf[0]);
       }
     };
+    // TR form of the fast path: the whole epilogue (alpha, bias, row bias, residual, mix) runs in fp32 on the
+    // accumulators themselves (residual / mix fetched in the accumulator layout, 8 bytes per lane and
+    // fragment), rounds once to bf16 and goes through a bf16 slab: half the LDS bytes of the fp32 slab,
+    // ds_write_b64 instead of four ds_write_b32, and the store phase is a plain 16-byte copy.
+    auto fast_epilogue_tr = [&](auto res_c, auto mix_c, auto rb_c) {
+      constexpr bool RES = decltype(res_c)::value, MIXB = decltype(mix_c)::value, RB = decltype(rb_c)::value;
+      constexpr int NF = TMQ * TNQ, EHL = SC + 8;               // bf16 slab row: SC + 16 B pad
+      constexpr int RPI = 64 / CPR, LPI = RPI * CPR, NIT = (SR + RPI - 1) / RPI;
+      constexpr int NRB = (RES && !MIXB) ? 2 : 1;
+      bf16_t* const eh = reinterpret_cast<bf16_t*>(et);
+      auto f_row = [&](int qm, int i) { return tile_m + qm * 128 + wr * SR + 16 * i + fr; };
+      auto f_col = [&](int qn, int j) { return tile_n + qn * (BN_ / 2) + wc * SC + 16 * j + 4 * fq; };
+      uint2 rbuf[NRB][NF], mbuf[NF];   // mbuf unused (and dropped) without a mix operand
+      // invalid (row, column) slots read the tensor's first element pair instead: loads stay unconditional
+      auto load_f = [&](const void* base, int ld, int qm, int qn, uint2 (&dst)[NF]) {
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            const int row = f_row(qm, i), col = f_col(qn, j);
+            const bool ok = row < p.M && col < p.N;
+            dst[i * TNQ + j] = *reinterpret_cast<const uint2*>((const bf16_t*)base + (ok ? (size_t)row * ld + col : 0));
+          }
+      };
+      auto to_slab = [&](int qm, int qn, const f32x4_t (&c)[TMQ][TNQ], const uint2 (&rq)[NF], const uint2 (&mq)[NF]) {
+        const int lc0 = qn * (BN_ / 2) + wc * SC;
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i) {
+          int img = 0;
+          if (RB) {
+            const int row = f_row(qm, i);
+            img = min(max(udiv22(row < p.M ? row : p.M - 1, p.rb_div) - rb_img0, 0), RB_IMG - 1);
+          }
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            const int lc = lc0 + 16 * j + 4 * fq;
+            const float4 b = *reinterpret_cast<const float4*>(&sbias[lc]);
+            float v[4] = {fmaf(c[i][j][0], p.alpha, b.x), fmaf(c[i][j][1], p.alpha, b.y),
+                          fmaf(c[i][j][2], p.alpha, b.z), fmaf(c[i][j][3], p.alpha, b.w)};
+            if (RB) {
+              const float4 q = *reinterpret_cast<const float4*>(&srb[img * BN_ + lc]);
+              v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+            }
+            if (RES) {
+              const uint2 t = rq[i * TNQ + j];
+              v[0] += __uint_as_float(t.x << 16); v[1] += __uint_as_float(t.x & 0xffff0000u);
+              v[2] += __uint_as_float(t.y << 16); v[3] += __uint_as_float(t.y & 0xffff0000u);
+            }
+            if (MIXB) {
+              const uint2 t = mq[i * TNQ + j];
+              const float m4[4] = {__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xffff0000u),
+                                   __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xffff0000u)};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = p.mix_alpha * m4[e] + (1.0f - p.mix_alpha) * v[e];
+            }
+            *reinterpret_cast<uint2*>(&eh[(16 * i + fr) * EHL + 16 * j + 4 * fq]) =
+                make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          }
+        }
+      };
+      const int r0 = lane / CPR, c8 = (lane - r0 * CPR) * 8;
+      auto from_slab = [&](int qm, int qn) {
+        const int rowf = tile_m + qm * 128 + wr * SR + r0, col = tile_n + qn * (BN_ / 2) + wc * SC + c8;
+        bf16_t* cp = (bf16_t*)p.C + (size_t)(rowf + p.orow_off) * p.ldc + col;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int r = r0 + it * RPI;
+          if (lane < LPI && r < SR && rowf + it * RPI < p.M && col < p.N)
+            *reinterpret_cast<uint4*>(cp + (size_t)it * RPI * p.ldc) = *reinterpret_cast<const uint4*>(&eh[r * EHL + c8]);
+        }
+      };
+      constexpr int QM[4] = {0, 0, 1, 1}, QN[4] = {0, 1, 0, 1};
+      if (RES && NRB == 2) load_f(p.R, p.ldr, 0, 0, rbuf[0]);
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        if (RES && NRB == 2 && qi + 1 < 4) load_f(p.R, p.ldr, QM[qi + 1], QN[qi + 1], rbuf[(qi + 1) % NRB]);
+        if (RES && NRB == 1) load_f(p.R, p.ldr, QM[qi], QN[qi], rbuf[0]);
+        if (MIXB) load_f(p.MIX, p.ldmix, QM[qi], QN[qi], mbuf);
+        to_slab(QM[qi], QN[qi], acc[QM[qi]][QN[qi]], rbuf[qi % NRB], mbuf);
+        from_slab(QM[qi], QN[qi]);     // wave-private slab: LDS ops of one wave complete in order
+      }
+    };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    if (fast) {
+    if (fast && TR) {
+      const int sel = (p.R ? 1 : 0) | (p.MIX ? 2 : 0) | (p.rowbias ? 4 : 0);
+      switch (sel) {
+        case 0: fast_epilogue_tr(F_{}, F_{}, F_{}); break;
+        case 1: fast_epilogue_tr(T_{}, F_{}, F_{}); break;
+        case 3: fast_epilogue_tr(T_{}, T_{}, F_{}); break;
+        case 4: fast_epilogue_tr(F_{}, F_{}, T_{}); break;
+        case 5: fast_epilogue_tr(T_{}, F_{}, T_{}); break;
+        default:
+          slab(acc[0][0]); flush(0, 0);
+          slab(acc[0][1]); flush(0, 1);
+          slab(acc[1][0]); flush(1, 0);
+          slab(acc[1][1]); flush(1, 1);
+      }
+    } else if (fast) {
       const int sel = (p.R ? 1 : 0) | (p.MIX ? 2 : 0) | (p.rowbias ? 4 : 0);
       switch (sel) {
         case 0: fast_epilogue(F_{}, F_{}, F_{}); break;
@@ -649,6 +753,15 @@ static void launch8p(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigne
                          vec_ok);
       return;
     }
+  }
+  if (G8_TR_ALL == 1 || (G8_TR_ALL == 2 && !d->R && !d->MIX)) {
+    if (d->amode == 1)
+      hipLaunchKernelGGL((gemm8p_kernel<BN_, 1, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+    else if (d->amode == 2)
+      hipLaunchKernelGGL((gemm8p_kernel<BN_, 2, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+    else
+      hipLaunchKernelGGL((gemm8p_kernel<BN_, 0, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+    return;
   }
   if (d->amode == 1)
     hipLaunchKernelGGL((gemm8p_kernel<BN_, 1>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);

@@ -213,6 +213,7 @@ class FamilyTimer:
 
     def __init__(self):
         self.ev = {}                         # family -> list of (e0, e1, work)
+        self.extra = {}                      # family -> summed secondary work (selective_scan: state updates)
 
     def _wrap(self, mod, name, fam, work_fn):
         orig = getattr(mod, name)
@@ -223,7 +224,11 @@ class FamilyTimer:
             e0.record()
             out = orig(*a, **k)
             e1.record()
-            self.ev.setdefault(fam, []).append((e0, e1, work_fn(*a, **k)))
+            w = work_fn(*a, **k)
+            if isinstance(w, tuple):          # (work, secondary count): the scan's state updates
+                w, extra = w
+                self.extra[fam] = self.extra.get(fam, 0) + extra
+            self.ev.setdefault(fam, []).append((e0, e1, w))
             return out
         setattr(mod, name, timed)
         self._restore.append((mod, name, orig))
@@ -238,10 +243,14 @@ class FamilyTimer:
 
         def w_scan(u, xdbl, *a, nb, L, R, n_keep, **k):
             D = u.shape[1]
-            return nb * L * D * 2 + nb * L * xdbl.shape[1] * xdbl.element_size() + 2 * nb * n_keep * D * 2
+            byts = nb * L * D * 2 + nb * L * xdbl.shape[1] * xdbl.element_size() + 2 * nb * n_keep * D * 2
+            # state updates h = exp(dt A) h + dt u B: 16 states per channel, forward direction up to the last
+            # kept token, reverse direction over all L tokens
+            return byts, nb * D * 16 * (n_keep + L)
 
         def w_scan2(a, b):
-            return sum(w_scan(**d) for d in (a, b))
+            ra, rb = w_scan(**a), w_scan(**b)
+            return ra[0] + rb[0], ra[1] + rb[1]
 
         def w_gn(x, *a, x2=None, residual=None, **k):
             C = x.shape[1] + (x2.shape[1] if x2 is not None else 0)
@@ -283,6 +292,16 @@ class FamilyTimer:
                             launches=len(evs), avg_launch_us=round(1000.0 * ms / len(evs), 1),
                             share_of_step=round(ms / step_ms_total, 4),
                             algorithmic_bytes_or_flop_per_launch=round(work / len(evs)))
+            if fam == "selective_scan" and fam in self.extra:
+                # the scan is VALU-issue bound, not HBM bound (PMC: ~5 cycles per VALU instruction, ~4.8 VALU
+                # instructions per state update): its compute floor is one v_exp per state update at the v_exp
+                # issue rate measured on gfx950 (tools/probes/valu_probe.hip: 4096 waves x 16384 v_exp in 0.239 ms)
+                upd = self.extra[fam] / len(evs)
+                floor_us = upd / V_EXP_PER_S * 1e6
+                out[fam]["exp_floor"] = dict(
+                    state_updates_per_launch=round(upd), v_exp_per_s=V_EXP_PER_S, floor_us=round(floor_us, 1),
+                    frac=round(floor_us / (1000.0 * ms / len(evs)), 4),
+                    source="profiles/r3_step18_valu_probe.txt (v_exp_f32, 4 waves / SIMD)")
             pmc = pmc_traffic(fam)
             if pmc:
                 # PMC bytes per kernel dispatch x dispatches per op call (GroupNorm: stats + apply)
@@ -291,6 +310,9 @@ class FamilyTimer:
                 out[fam]["traffic_unit"] = "HBM bytes per op call (PMC 2*FETCH_SIZE + WRITE_SIZE)"
                 out[fam]["traffic_source"] = pmc.get("source")
         return out
+
+
+V_EXP_PER_S = 4096 * 16384 * 64 / 0.239e-3      # gfx950 v_exp_f32 issue rate, all 1024 SIMDs (valu_probe)
 
 
 def cpu_baseline(unet, H, W, frames=2, mode=0):

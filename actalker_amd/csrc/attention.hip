@@ -30,6 +30,29 @@ typedef __attribute__((address_space(3))) void lds_void;
 //  * P never leaves registers: S^T's accumulator rows are the B operand of the P.V product.
 
 #define FA_TILE 8192            // 64 keys x 128 B
+// long-sequence configuration (Sq >= 2048): waves per block and 32-query groups per wave
+#ifndef FA_BIG_NW
+#define FA_BIG_NW 8
+#endif
+#ifndef FA_BIG_QG
+#define FA_BIG_QG 1
+#endif
+// 1: no per-tile max search; the tile's bf16 P sum bounds every p (FA_LSUM_MAX), the max is taken only
+// when that bound is exceeded. 0: max search on every tile (p <= 2^FA_DEFER)
+#ifndef FA_SUM_CHECK
+#define FA_SUM_CHECK 1
+#endif
+#define FA_LSUM_MAX 65536.0f
+// 1: flash16_kernel (v_mfma_f32_16x16x32_bf16) for every flash launch; 0: flash_attn_kernel (32x32x16)
+#ifndef FA_M16
+#define FA_M16 1
+#endif
+#ifndef FA16_PRIO
+#define FA16_PRIO 0
+#endif
+#ifndef FA16_BIG_NW
+#define FA16_BIG_NW 8
+#endif
 #ifndef FA_PRIO
 #define FA_PRIO 0
 #endif
@@ -59,10 +82,13 @@ struct FaIpEpi {
   int S;
 };
 
-// NW waves per block (32 queries each) share every K/V tile.
-template <int NW, bool IP>
-__global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDesc p, unsigned k_bytes,
-                                                                unsigned v_bytes, const FaIpEpi ip) {
+// NW waves per block share every K/V tile; each wave owns QG groups of 32 queries. QG = 2 halves the LDS
+// fragment reads per MFMA (every K / V fragment a wave reads feeds both query groups) at twice the
+// accumulator registers per wave (2 waves per SIMD instead of 4).
+template <int NW, bool IP, int QG = 1>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG, 4 / QG))) void flash_attn_kernel(const ActhAttnDesc p,
+                                                                                 unsigned k_bytes, unsigned v_bytes,
+                                                                                 const FaIpEpi ip) {
   __shared__ __attribute__((aligned(16))) char smem[4 * FA_TILE];   // [buf][K | V]
   constexpr int PPW = 8 / NW;                    // DMA pieces (8 rows) per wave per tile and operand
 
@@ -86,7 +112,7 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
     h = (lin / nq) % nh;
     bat = lin / (nq * nh);
   }
-  const int q = qblk * (32 * NW) + wave * 32 + r32;
+  const int q0 = qblk * (32 * NW * QG) + wave * (32 * QG) + r32;   // query of group g: q0 + 32 g
   const bf16_t* qb = (const bf16_t*)p.q + bat * p.bsq + h * 64;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>((const bf16_t*)p.k + bat * p.bsk + h * 64), (short)0, (int)k_bytes, 0x00020000);
@@ -96,18 +122,21 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
   // Q^T fragments as the B operand: lane holds Q[q][16s + 8hh + j], prescaled by c = scale * log2(e)
   // (rounded to bf16) so the S^T accumulators are scores in log2 units
   const float c = p.scale * 1.4426950408889634f;
-  bf16x8_t qf[4];
+  bf16x8_t qf[QG][4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    uint4 t = make_uint4(0, 0, 0, 0);
-    if (q < p.Sq) t = *reinterpret_cast<const uint4*>(qb + (size_t)q * p.ldq + 16 * s + 8 * hh);
-    const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
-    uint32_t w[4];
+  for (int g = 0; g < QG; ++g)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      w[j] = pack2(__uint_as_float(tw[j] << 16) * c, __uint_as_float(tw[j] & 0xffff0000u) * c);
-    qf[s] = *reinterpret_cast<bf16x8_t*>(w);
-  }
+    for (int s = 0; s < 4; ++s) {
+      const int q = q0 + 32 * g;
+      uint4 t = make_uint4(0, 0, 0, 0);
+      if (q < p.Sq) t = *reinterpret_cast<const uint4*>(qb + (size_t)q * p.ldq + 16 * s + 8 * hh);
+      const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = pack2(__uint_as_float(tw[j] << 16) * c, __uint_as_float(tw[j] & 0xffff0000u) * c);
+      qf[g][s] = *reinterpret_cast<bf16x8_t*>(w);
+    }
 
   // DMA: wave w fills rows [8(w + NW u), +8) of each tile; lane -> (row, physical 16-B slot
   // lane & 7) holding logical chunk slot ^ swizzle(row)
@@ -140,17 +169,21 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
   // The first tile always sets m. Per score the common path costs half a v_max3, one v_exp, one add
   // and half a v_cvt_pk (the textbook loop adds an FMA per score and a rescale per max increase).
   constexpr float FA_DEFER = 8.0f;
-  f32x16_t negm, o0, o1;
-  float l_run = 0.0f;
+  f32x16_t negm[QG], o[QG][2];
+  float l_run[QG];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { negm[r] = 0.0f; o0[r] = 0.0f; o1[r] = 0.0f; }
+  for (int g = 0; g < QG; ++g) {
+    l_run[g] = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { negm[g][r] = 0.0f; o[g][0][r] = 0.0f; o[g][1][r] = 0.0f; }
+  }
 
-  // V transpose-read addressing: lane group g = lane / 16 covers d block (g & 1) * 16 (+32 for o1)
-  // and keys 8 * rd + 4 * (g >> 1) + qq of the 16-key step (the k order of S^T's accumulator rows,
+  // V transpose-read addressing: lane group tg = lane / 16 covers d block (tg & 1) * 16 (+32 for o[.][1])
+  // and keys 8 * rd + 4 * (tg >> 1) + tq of the 16-key step (the k order of S^T's accumulator rows,
   // which are the B operand: element j of lane half h is key 8 * (j >> 2) + 4h + (j & 3)); lane
-  // 4qq + pp of the group supplies row qq, columns 4pp..4pp+3
+  // 4tq + tp of the group supplies row tq, columns 4tp..4tp+3
   const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
-  const int tdcol = (tg & 1) * 16 + 4 * tp;          // d of this lane's 8-byte piece (o0)
+  const int tdcol = (tg & 1) * 16 + 4 * tp;          // d of this lane's 8-byte piece (o[.][0])
 
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -171,58 +204,135 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
 #pragma unroll
       for (int s = 0; s < 4; ++s) kf[sub][s] = *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4));
     }
-    f32x16_t st[2];
+    f32x16_t st[QG][2];
     FA_PRIO_ON();
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        st[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[sub][s], qf[s], s == 0 ? negm : st[sub], 0, 0, 0);
+      for (int g = 0; g < QG; ++g)
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+          st[g][sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[sub][s], qf[g][s], s == 0 ? negm[g] : st[g][sub],
+                                                               0, 0, 0);
     FA_PRIO_OFF();
     if (FA_LATE_DMA && kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
     if (kv0 + 64 > p.Skv) {
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+      for (int g = 0; g < QG; ++g)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) st[sub][r] = -INFINITY;
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) st[g][sub][r] = -INFINITY;
     }
     // ---- softmax numerators (lane = query column) ----
-    float mx = st[0][0];
+    bf16x8_t pf[QG][2][2];
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+    for (int g = 0; g < QG; ++g) {
+      float ls;
+#if FA_SUM_CHECK
+      // common path: no max search. p = exp2(s c - m) packed to bf16 and summed (v_dot2 on the packed
+      // pairs: l accumulates exactly the bf16 weights the P.V product uses); every p <= the lane's tile sum,
+      // so a sum <= FA_LSUM_MAX bounds them all and m needs no update. Otherwise (and always on the first
+      // tile, which sets m) the exact max is taken and the tile is exponentiated again.
+      auto expack = [&]() {
+        const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+        float l0 = 0.0f, l1 = 0.0f;
 #pragma unroll
-      for (int r = (sub == 0 ? 1 : 0); r < 16; ++r) mx = fmaxf(mx, st[sub][r]);
-    {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    if (kv0 == 0 || __any(!(mx <= FA_DEFER))) {    // rare: raise m (NaN-safe test)
-      const float dm = kv0 == 0 ? mx : fmaxf(mx, 0.0f);
-      if (kv0 > 0) {
-        const float alpha = __builtin_amdgcn_exp2f(-dm);
-        l_run *= alpha;
+        for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-      }
+          for (int s2 = 0; s2 < 2; ++s2) {
+            uint32_t w[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { negm[r] -= dm; st[0][r] -= dm; st[1][r] -= dm; }
-    }
-    bf16x8_t pf[2][2];
+            for (int j = 0; j < 4; ++j) {
+              w[j] = pack2(__builtin_amdgcn_exp2f(st[g][sub][8 * s2 + 2 * j]),
+                           __builtin_amdgcn_exp2f(st[g][sub][8 * s2 + 2 * j + 1]));
+              const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[j]);
+              if (j & 1) l1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l1, false);
+              else l0 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l0, false);
+            }
+            pf[g][sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
+          }
+        return l0 + l1;
+      };
+      ls = expack();
+      if (kv0 == 0 || __any(!(ls <= FA_LSUM_MAX))) {    // rare: raise m (NaN-safe test)
+        // S^T again from the K tile still in LDS (st need not stay live through the common path)
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+        for (int sub = 0; sub < 2; ++sub) {
+          const int key = sub * 32 + r32;
+          const char* kr = kt + key * 128;
+          const int sk = fa_swk(key);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        uint32_t w[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float p0 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j]);
-          const float p1 = __builtin_amdgcn_exp2f(st[sub][8 * s2 + 2 * j + 1]);
-          l_run += p0 + p1;
-          w[j] = pack2(p0, p1);
+          for (int s = 0; s < 4; ++s)
+            st[g][sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4)), qf[g][s],
+                s == 0 ? negm[g] : st[g][sub], 0, 0, 0);
         }
-        pf[sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
+        if (kv0 + 64 > p.Skv) {
+#pragma unroll
+          for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kv0 + sub * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Skv) st[g][sub][r] = -INFINITY;
+        }
+        float mx = st[g][0][0];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = (sub == 0 ? 1 : 0); r < 16; ++r) mx = fmaxf(mx, st[g][sub][r]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        const float dm = kv0 == 0 ? mx : fmaxf(mx, 0.0f);
+        if (kv0 > 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-dm);
+          l_run[g] *= alpha;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) { o[g][0][r] *= alpha; o[g][1][r] *= alpha; }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { negm[g][r] -= dm; st[g][0][r] -= dm; st[g][1][r] -= dm; }
+        ls = expack();
       }
+#else
+      float mx = st[g][0][0];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = (sub == 0 ? 1 : 0); r < 16; ++r) mx = fmaxf(mx, st[g][sub][r]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
+      if (kv0 == 0 || __any(!(mx <= FA_DEFER))) {    // rare: raise m (NaN-safe test)
+        const float dm = kv0 == 0 ? mx : fmaxf(mx, 0.0f);
+        if (kv0 > 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-dm);
+          l_run[g] *= alpha;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) { o[g][0][r] *= alpha; o[g][1][r] *= alpha; }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { negm[g][r] -= dm; st[g][0][r] -= dm; st[g][1][r] -= dm; }
+      }
+      ls = 0.0f;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float p0 = __builtin_amdgcn_exp2f(st[g][sub][8 * s2 + 2 * j]);
+            const float p1 = __builtin_amdgcn_exp2f(st[g][sub][8 * s2 + 2 * j + 1]);
+            ls += p0 + p1;
+            w[j] = pack2(p0, p1);
+          }
+          pf[g][sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
+        }
+#endif
+      l_run[g] += ls;
+    }
     // ---- O^T += V^T P^T: A operand (d rows x 16 keys) by transpose reads of row-major V ----
     FA_PRIO_ON();
 #pragma unroll
@@ -247,8 +357,9 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
           typedef short short8_t __attribute__((ext_vector_type(8)));
           short8_t v8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           const bf16x8_t af = *reinterpret_cast<bf16x8_t*>(&v8);
-          if (dh == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[sub][s2], o0, 0, 0, 0);
-          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[sub][s2], o1, 0, 0, 0);
+#pragma unroll
+          for (int g = 0; g < QG; ++g)
+            o[g][dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[g][sub][s2], o[g][dh], 0, 0, 0);
         }
       }
     FA_PRIO_OFF();
@@ -258,49 +369,304 @@ __global__ __launch_bounds__(NW * 64, 2) void flash_attn_kernel(const ActhAttnDe
     buf ^= 1;
   }
 
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (q >= p.Sq) return;
-  float inv = 1.0f / l_run;
-  bf16_t* ob = (bf16_t*)p.o + bat * p.bso + (size_t)q * p.ldo + h * 64;
-  float wa = 0.0f, wb = 0.0f;
-  const bf16_t* vbr = nullptr;
-  const bf16_t* vbb = nullptr;
-  if (IP) {
-    const int s = q % ip.S;
-    inv *= ip.sa * (ip.ma ? ip.ma[s] : 1.0f);
-    vbr = ip.vbase + (size_t)bat * ip.ldvbase + h * 64;
-    if (ip.vb) {
-      wb = ip.sb * (ip.mb ? ip.mb[s] : 1.0f);
-      vbb = ip.vb + (size_t)bat * ip.ldvb + h * 64;
-    }
-  }
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d0 = 8 * g + 4 * hh;
-    float a[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { a[e] = o0[4 * g + e] * inv; a[4 + e] = o1[4 * g + e] * inv; }
+  for (int g = 0; g < QG; ++g) {
+    const float lr = l_run[g] + __shfl_xor(l_run[g], 32, 64);
+    const int q = q0 + 32 * g;
+    if (q >= p.Sq) continue;
+    float inv = 1.0f / lr;
+    bf16_t* ob = (bf16_t*)p.o + bat * p.bso + (size_t)q * p.ldo + h * 64;
+    float wb = 0.0f;
+    const bf16_t* vbr = nullptr;
+    const bf16_t* vbb = nullptr;
     if (IP) {
-      // + vbase (+ wb * vb): 4 columns at d0 and 4 at 32 + d0
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const uint2 bw = *reinterpret_cast<const uint2*>(vbr + 32 * half + d0);
-        a[4 * half + 0] += __uint_as_float(bw.x << 16); a[4 * half + 1] += __uint_as_float(bw.x & 0xffff0000u);
-        a[4 * half + 2] += __uint_as_float(bw.y << 16); a[4 * half + 3] += __uint_as_float(bw.y & 0xffff0000u);
-        if (vbb) {
-          const uint2 cw = *reinterpret_cast<const uint2*>(vbb + 32 * half + d0);
-          a[4 * half + 0] = fmaf(wb, __uint_as_float(cw.x << 16), a[4 * half + 0]);
-          a[4 * half + 1] = fmaf(wb, __uint_as_float(cw.x & 0xffff0000u), a[4 * half + 1]);
-          a[4 * half + 2] = fmaf(wb, __uint_as_float(cw.y << 16), a[4 * half + 2]);
-          a[4 * half + 3] = fmaf(wb, __uint_as_float(cw.y & 0xffff0000u), a[4 * half + 3]);
-        }
+      const int s = q % ip.S;
+      inv *= ip.sa * (ip.ma ? ip.ma[s] : 1.0f);
+      vbr = ip.vbase + (size_t)bat * ip.ldvbase + h * 64;
+      if (ip.vb) {
+        wb = ip.sb * (ip.mb ? ip.mb[s] : 1.0f);
+        vbb = ip.vb + (size_t)bat * ip.ldvb + h * 64;
       }
     }
-    uint2 w0, w1;
-    w0.x = pack2(a[0], a[1]); w0.y = pack2(a[2], a[3]);
-    w1.x = pack2(a[4], a[5]); w1.y = pack2(a[6], a[7]);
-    *reinterpret_cast<uint2*>(ob + d0) = w0;
-    *reinterpret_cast<uint2*>(ob + 32 + d0) = w1;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int d0 = 8 * gg + 4 * hh;
+      float a[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { a[e] = o[g][0][4 * gg + e] * inv; a[4 + e] = o[g][1][4 * gg + e] * inv; }
+      if (IP) {
+        // + vbase (+ wb * vb): 4 columns at d0 and 4 at 32 + d0
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const uint2 bw = *reinterpret_cast<const uint2*>(vbr + 32 * half + d0);
+          a[4 * half + 0] += __uint_as_float(bw.x << 16); a[4 * half + 1] += __uint_as_float(bw.x & 0xffff0000u);
+          a[4 * half + 2] += __uint_as_float(bw.y << 16); a[4 * half + 3] += __uint_as_float(bw.y & 0xffff0000u);
+          if (vbb) {
+            const uint2 cw = *reinterpret_cast<const uint2*>(vbb + 32 * half + d0);
+            a[4 * half + 0] = fmaf(wb, __uint_as_float(cw.x << 16), a[4 * half + 0]);
+            a[4 * half + 1] = fmaf(wb, __uint_as_float(cw.x & 0xffff0000u), a[4 * half + 1]);
+            a[4 * half + 2] = fmaf(wb, __uint_as_float(cw.y << 16), a[4 * half + 2]);
+            a[4 * half + 3] = fmaf(wb, __uint_as_float(cw.y & 0xffff0000u), a[4 * half + 3]);
+          }
+        }
+      }
+      uint2 w0, w1;
+      w0.x = pack2(a[0], a[1]); w0.y = pack2(a[2], a[3]);
+      w1.x = pack2(a[4], a[5]); w1.y = pack2(a[6], a[7]);
+      *reinterpret_cast<uint2*>(ob + d0) = w0;
+      *reinterpret_cast<uint2*>(ob + 32 + d0) = w1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// The same flash attention on v_mfma_f32_16x16x32_bf16 (per wave 32 queries = 2 query blocks of 16;
+// per 64-key tile 4 key blocks): the MI355X holds a higher clock on the 16x16 shape under sustained
+// load at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS item 7). Layouts:
+//  * S^T[key block kb][query block qb] (4 accumulators per lane: keys 16 kb + 4 g + r, query 16 qb +
+//    (lane & 15), g = lane >> 4) = K Q^T - m, A = K rows (16 keys x 32 d, ds_read_b128 of chunk 4 ks + g),
+//    B = Q^T (lane: query lane & 15, d 32 ks + 8 g .. + 7).
+//  * P^T as the PV product's B operand needs no data movement: for the 32-key step t the lane's 8 k values
+//    are keys 32 t + 4 g + 0..3 (S^T[2t]) and 32 t + 16 + 4 g + 0..3 (S^T[2t + 1]); the V^T A operand is
+//    read in that same key order by two ds_read_b64_tr_b16 (4 keys x 16 d each; the 16 lanes of group g
+//    supply keys 32 t (+16) + 4 g + (lane & 15) / 4, d 16 db + 4 (lane & 3)).
+//  * V chunks are swizzled by ((key >> 1) & 3) << 1 (even, so a 32-byte d slice stays whole): the 16 keys
+//    x 32 bytes of one transpose read land on distinct banks.
+//  * Softmax without a per-tile max search (FA_SUM_CHECK scheme, above); row sums are lane-partial
+//    (4 lanes per query) until the end.
+__device__ __forceinline__ int fa_swv16(int key) { return ((key >> 1) & 3) << 1; }
+
+template <int NW, bool IP>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4))) void flash16_kernel(
+    const ActhAttnDesc p, unsigned k_bytes, unsigned v_bytes, const FaIpEpi ip) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * FA_TILE];   // [buf][K | V]
+  constexpr int PPW = 8 / NW;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  int qblk, h, bat;
+  {
+    const int nq = gridDim.x, nh = gridDim.y;
+    const int nwg = nq * nh * (int)gridDim.z;
+    const int bid = blockIdx.x + nq * (blockIdx.y + nh * blockIdx.z);
+    const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    qblk = lin % nq;
+    h = (lin / nq) % nh;
+    bat = lin / (nq * nh);
+  }
+  const int q0 = qblk * (32 * NW) + wave * 32 + l16;     // query of block qb: q0 + 16 qb
+  const bf16_t* qb_ = (const bf16_t*)p.q + bat * p.bsq + h * 64;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((const bf16_t*)p.k + bat * p.bsk + h * 64), (short)0, (int)k_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((const bf16_t*)p.v + bat * p.bsv + h * 64), (short)0, (int)v_bytes, 0x00020000);
+
+  const float c = p.scale * 1.4426950408889634f;
+  bf16x8_t qf[2][2];                                    // [qb][ks]
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int q = q0 + 16 * qb;
+      uint4 t = make_uint4(0, 0, 0, 0);
+      if (q < p.Sq) t = *reinterpret_cast<const uint4*>(qb_ + (size_t)q * p.ldq + 32 * ks + 8 * g);
+      const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = pack2(__uint_as_float(tw[j] << 16) * c, __uint_as_float(tw[j] & 0xffff0000u) * c);
+      qf[qb][ks] = *reinterpret_cast<bf16x8_t*>(w);
+    }
+
+  const int lrow = lane >> 3, slot = lane & 7;
+  int krow[PPW], kch[PPW], vch[PPW];
+#pragma unroll
+  for (int u = 0; u < PPW; ++u) {
+    krow[u] = (wave + NW * u) * 8 + lrow;
+    kch[u] = slot ^ fa_swk(krow[u]);
+    vch[u] = slot ^ fa_swv16(krow[u]);
+  }
+  auto stage = [&](int kv0, int buf) {
+    char* kt = smem + buf * 2 * FA_TILE;
+    char* vt = kt + FA_TILE;
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int key = kv0 + krow[u];
+      const unsigned ko = key < p.Skv ? ((unsigned)key * p.ldk + kch[u] * 8) * 2u : 0x80000000u;
+      const unsigned vo = key < p.Skv ? ((unsigned)key * p.ldv + vch[u] * 8) * 2u : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(kt + (wave + NW * u) * 1024), 16, ko, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void*)(vt + (wave + NW * u) * 1024), 16, vo, 0, 0, 0);
+    }
+  };
+
+  f32x4_t negm[2], o[4][2];                            // o[db][qb]: d 16 db + 4 g + r, query 16 qb + l16
+  float l_run[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    negm[0][r] = 0.0f; negm[1][r] = 0.0f;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) { o[db][0][r] = 0.0f; o[db][1][r] = 0.0f; }
+  }
+  // K fragment offsets (k step ks; key block kb adds 2048 kb: the swizzle of key 16 kb + l16 is that of l16)
+  // and V transpose-read offsets (d block db; key step t / half add 4096 t + 2048 half), buffer-relative
+  int koff[2], voff[4];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) koff[ks] = l16 * 128 + (((4 * ks + g) ^ fa_swk(l16)) << 4);
+  {
+    const int tq = l16 >> 2, tp = l16 & 3, vkey = 4 * g + tq;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int d = 16 * db + 4 * tp;
+      voff[db] = vkey * 128 + (((d >> 3) ^ fa_swv16(vkey)) << 4) + (d & 7) * 2;
+    }
+  }
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (FA16_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // static priority for the younger half
+  int buf = 0;
+  for (int kv0 = 0; kv0 < p.Skv; kv0 += 64) {
+    if (kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
+    const char* kt = smem + buf * 2 * FA_TILE;
+    const char* vt = kt + FA_TILE;
+
+    // ---- S^T = K Q^T - m ----
+    f32x4_t st[2][4];                                   // [qb][kb]
+    {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kt + koff[ks] + 2048 * kb);
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][ks], ks == 0 ? negm[qb] : st[qb][kb],
+                                                                0, 0, 0);
+        }
+      if (kv0 + 64 > p.Skv) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (kv0 + 16 * kb + 4 * g + r >= p.Skv) st[qb][kb][r] = -INFINITY;
+      }
+    }
+    // ---- softmax numerators: P^T B operands pf[t][qb] (keys 32 t + 4 g + 0..3, 32 t + 16 + 4 g + 0..3) ----
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      auto expack = [&]() {
+        const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+        float l0 = 0.0f, l1 = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4_t& sv = st[qb][2 * t + (j >> 1)];
+            w[j] = pack2(__builtin_amdgcn_exp2f(sv[2 * (j & 1)]), __builtin_amdgcn_exp2f(sv[2 * (j & 1) + 1]));
+            const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[j]);
+            if (j & 1) l1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l1, false);
+            else l0 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l0, false);
+          }
+          pf[t][qb] = *reinterpret_cast<bf16x8_t*>(w);
+        }
+        return l0 + l1;
+      };
+      float ls = expack();
+      if (kv0 == 0 || __any(!(ls <= FA_LSUM_MAX))) {    // rare: raise m (NaN-safe test)
+        float mx = st[qb][0][0];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, st[qb][kb][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float dm = kv0 == 0 ? mx : fmaxf(mx, 0.0f);
+        if (kv0 > 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-dm);
+          l_run[qb] *= alpha;
+#pragma unroll
+          for (int db = 0; db < 4; ++db)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[db][qb][r] *= alpha;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          negm[qb][r] -= dm;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) st[qb][kb][r] -= dm;
+        }
+        ls = expack();
+      }
+      l_run[qb] += ls;
+    }
+    // ---- O^T += V^T P^T ----
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        short4_t rd2[2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+          rd2[half] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(vt + voff[db] + 4096 * t + 2048 * half));
+        typedef short short8_t __attribute__((ext_vector_type(8)));
+        const short8_t v8 = {rd2[0][0], rd2[0][1], rd2[0][2], rd2[0][3], rd2[1][0], rd2[1][1], rd2[1][2], rd2[1][3]};
+        const bf16x8_t af = __builtin_bit_cast(bf16x8_t, v8);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, pf[t][qb], o[db][qb], 0, 0, 0);
+      }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    buf ^= 1;
+  }
+
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float lr = l_run[qb] + __shfl_xor(l_run[qb], 16, 64);
+    lr += __shfl_xor(lr, 32, 64);
+    const int q = q0 + 16 * qb;
+    if (q >= p.Sq) continue;
+    float inv = 1.0f / lr;
+    bf16_t* ob = (bf16_t*)p.o + bat * p.bso + (size_t)q * p.ldo + h * 64;
+    float wb = 0.0f;
+    const bf16_t* vbr = nullptr;
+    const bf16_t* vbb = nullptr;
+    if (IP) {
+      const int s = q % ip.S;
+      inv *= ip.sa * (ip.ma ? ip.ma[s] : 1.0f);
+      vbr = ip.vbase + (size_t)bat * ip.ldvbase + h * 64;
+      if (ip.vb) {
+        wb = ip.sb * (ip.mb ? ip.mb[s] : 1.0f);
+        vbb = ip.vb + (size_t)bat * ip.ldvb + h * 64;
+      }
+    }
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int d0 = 16 * db + 4 * g;
+      float a[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = o[db][qb][r] * inv;
+      if (IP) {
+        const uint2 bw = *reinterpret_cast<const uint2*>(vbr + d0);
+        a[0] += __uint_as_float(bw.x << 16); a[1] += __uint_as_float(bw.x & 0xffff0000u);
+        a[2] += __uint_as_float(bw.y << 16); a[3] += __uint_as_float(bw.y & 0xffff0000u);
+        if (vbb) {
+          const uint2 cw = *reinterpret_cast<const uint2*>(vbb + d0);
+          a[0] = fmaf(wb, __uint_as_float(cw.x << 16), a[0]);
+          a[1] = fmaf(wb, __uint_as_float(cw.x & 0xffff0000u), a[1]);
+          a[2] = fmaf(wb, __uint_as_float(cw.y << 16), a[2]);
+          a[3] = fmaf(wb, __uint_as_float(cw.y & 0xffff0000u), a[3]);
+        }
+      }
+      *reinterpret_cast<uint2*>(ob + d0) = make_uint2(pack2(a[0], a[1]), pack2(a[2], a[3]));
+    }
   }
 }
 
@@ -313,10 +679,21 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
   const long long kb = ((long long)(d->Skv - 1) * d->ldk + 64) * 2, vb = ((long long)(d->Skv - 1) * d->ldv + 64) * 2;
   if (kb >= 0x80000000LL || vb >= 0x80000000LL) return ACTH_EINVAL;
   const FaIpEpi none = {};
-  if (d->Sq >= 2048) {
-    dim3 grid((d->Sq + 255) / 256, d->nheads, d->nbatch);
-    hipLaunchKernelGGL((flash_attn_kernel<8, false>), grid, dim3(512), 0, stream, *d, (unsigned)kb, (unsigned)vb,
-                       none);
+  if (FA_M16) {
+    if (d->Sq >= 2048) {
+      constexpr int nq = FA16_BIG_NW * 32;
+      dim3 grid((d->Sq + nq - 1) / nq, d->nheads, d->nbatch);
+      hipLaunchKernelGGL((flash16_kernel<FA16_BIG_NW, false>), grid, dim3(FA16_BIG_NW * 64), 0, stream, *d,
+                         (unsigned)kb, (unsigned)vb, none);
+    } else {
+      dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
+      hipLaunchKernelGGL((flash16_kernel<4, false>), grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb, none);
+    }
+  } else if (d->Sq >= 2048) {
+    constexpr int nq = FA_BIG_NW * 32 * FA_BIG_QG;
+    dim3 grid((d->Sq + nq - 1) / nq, d->nheads, d->nbatch);
+    hipLaunchKernelGGL((flash_attn_kernel<FA_BIG_NW, false, FA_BIG_QG>), grid, dim3(FA_BIG_NW * 64), 0, stream, *d,
+                       (unsigned)kb, (unsigned)vb, none);
   } else {
     dim3 grid((d->Sq + 127) / 128, d->nheads, d->nbatch);
     hipLaunchKernelGGL((flash_attn_kernel<4, false>), grid, dim3(256), 0, stream, *d, (unsigned)kb, (unsigned)vb,
@@ -550,7 +927,13 @@ extern "C" int acth_ip_attn(const ActhIpAttnDesc* d, hipStream_t stream) {
     ep.vb = (const bf16_t*)d->vb; ep.ldvb = d->ldvb;
     ep.ma = d->mask_a; ep.mb = d->mask_b; ep.sa = d->sa; ep.sb = d->sb; ep.S = d->S;
     const long long kb = ((long long)(d->nkeys - 1) * d->ldkv + 64) * 2;
-    if (a.Sq >= 2048) {
+    if (FA_M16 && a.Sq >= 2048) {
+      dim3 grid((a.Sq + 255) / 256, a.nheads, a.nbatch);
+      hipLaunchKernelGGL((flash16_kernel<8, true>), grid, dim3(512), 0, stream, a, (unsigned)kb, (unsigned)kb, ep);
+    } else if (FA_M16) {
+      dim3 grid((a.Sq + 127) / 128, a.nheads, a.nbatch);
+      hipLaunchKernelGGL((flash16_kernel<4, true>), grid, dim3(256), 0, stream, a, (unsigned)kb, (unsigned)kb, ep);
+    } else if (a.Sq >= 2048) {
       dim3 grid((a.Sq + 255) / 256, a.nheads, a.nbatch);
       hipLaunchKernelGGL((flash_attn_kernel<8, true>), grid, dim3(512), 0, stream, a, (unsigned)kb, (unsigned)kb, ep);
     } else {

@@ -1,6 +1,7 @@
 """Per-UNet-call kernel time by (kernel, grid) from a rocprofv3 --kernel-trace CSV: which dispatch shapes
 hold the step (grid x in workgroups, grid y); calls are normalised by the number of level-0 spatial
-attention dispatches (10 flash_attn_kernel<8, false> per UNet call at 576x1024).
+attention dispatches (10 flash16_kernel<8, false> -- flash_attn_kernel<8, false> before round 3 step 28 -- per UNet
+call at 576x1024).
 
   python tools/trace_by_grid.py gpurun_out/<dir>/run_kernel_trace.csv|run_results.db [--top 45] [--filter gn_]
 """
@@ -30,7 +31,7 @@ def main():
         k = (n, gx, gy)
         agg[k][0] += 1
         agg[k][1] += us
-    calls = sum(v[0] for k, v in agg.items() if k[0] == "flash_attn_kernel<8, false>") / 10
+    calls = sum(v[0] for k, v in agg.items() if k[0] in ("flash_attn_kernel<8, false>", "flash16_kernel<8, false>")) / 10
     tot = sum(v[1] for v in agg.values()) / calls
     print(f"UNet calls {calls:.0f}; kernel ms per call {tot / 1e3:.1f}")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:

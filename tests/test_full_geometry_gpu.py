@@ -177,7 +177,7 @@ def test_pipeline_25_steps_matches_oracle(dev, loop_unet, mode):
     assert st["rel_l2"] < 3e-2, st
 
 
-@pytest.mark.parametrize("mode", ["mode0"])
+@pytest.mark.parametrize("mode", ["mode0", "mode2"])
 def test_pipeline_25_steps_real_width_matches_oracle(dev, full_unet, mode):
     """The same 25-step windowed 4-way-CFG loop on the REAL-WIDTH UNet (320 / 640 / 1280 / 1280 channels,
     synthetic weights of the full-geometry cases) at a 16x32 latent, vs the fp32 oracle loop

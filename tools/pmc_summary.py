@@ -36,7 +36,7 @@ def main():
         import json
         out = sys.argv[sys.argv.index("--json") + 1]
         src = sys.argv[sys.argv.index("--source") + 1] if "--source" in sys.argv else d
-        fams = {"acth_gemm": lambda k: "gemm" in k, "flash_attn": lambda k: "flash_attn" in k,
+        fams = {"acth_gemm": lambda k: "gemm" in k, "flash_attn": lambda k: "flash_attn" in k or "flash16" in k,
                 "selective_scan": lambda k: "scan" in k, "groupnorm": lambda k: k.startswith("gn_"),
                 "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k}
         res = {}

@@ -23,6 +23,17 @@
 
 using namespace gemm;
 
+// 1: 3x3-conv K order with the 64-channel slice outer and the tap inner (L2 reuse of the nine taps'
+// shared window). Measured slower in isolation (level-0 conv 951 -> 881 TFLOP/s, level 2 1106 -> 945,
+// profiles/r3_step31_conv_order_rejected.log), so off
+#ifndef G8_CONV_CMAJOR
+#define G8_CONV_CMAJOR 0
+#endif
+// 1: 3x3-conv rows (no upsample) carry their tap-(0, 0) pixel and a 9-bit in-image tap mask
+#ifndef G8_TAP_MASK
+#define G8_TAP_MASK 1
+#endif
+
 namespace {
 
 // A row's source coordinates packed into two registers (four rows per wave stay live across the whole
@@ -36,7 +47,19 @@ template <int AMODE>
 __device__ __forceinline__ RowPk pack_row(const ActhGemmDesc& p, int m) {
   const RowInfo ri = row_info(p, m);
   RowPk r;
-  if (AMODE == 1) {
+  if (AMODE == 1 && G8_TAP_MASK && !p.upsample) {
+    // a = input pixel index of tap (0, 0) (may be negative), b = 9-bit mask of the taps inside the image
+    // (-1 past M): a tap's pixel is then a + (tap / 3) W + tap % 3, one add and a bit test per row
+    const int iy0 = ri.y * p.conv_stride - 1, ix0 = ri.x * p.conv_stride - 1;
+    int mask = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = iy0 + t / 3, ix = ix0 + t % 3;
+      if (iy >= 0 && ix >= 0 && iy < p.H && ix < p.W) mask |= 1 << t;
+    }
+    r.a = (ri.b * p.H + iy0) * p.W + ix0;
+    r.b = ri.ok ? mask : -1;
+  } else if (AMODE == 1) {
     r.a = (ri.y << 16) | ri.x;
     r.b = ri.ok ? ri.b : -1;
   } else {
@@ -53,6 +76,11 @@ __device__ __forceinline__ int tap_pixel8(const ActhGemmDesc& p, const RowPk& ri
   RowPk r = rin;
   asm volatile("" : "+v"(r.a), "+v"(r.b));
   if (AMODE == 0) return r.a;
+  if (AMODE == 1 && G8_TAP_MASK && !p.upsample) {
+    if (r.b < 0 || !((r.b >> tap) & 1)) return -1;
+    const int ky = tap / 3;
+    return r.a + ky * p.W + (tap - 3 * ky);
+  }
   if (AMODE == 1) {
     if (r.b < 0) return -1;
     const int y = r.a >> 16, x = r.a & 0xffff;
@@ -203,12 +231,23 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
 
   // per-K-tile staging parameters, advanced by prep_k() in K order
   int s_tap = 0, s_c0 = 0;
-  int k_c0 = 0, k_k0 = 0;
+  int k_c0 = 0, k_k0 = 0, k_kb = 0;
   bool k_second = false, k_tail = false;
+  const int ntap = AMODE == 0 ? 1 : p.K / cin;
   auto prep_k = [&](int kt) {
     k_k0 = kt * 64;
+    k_kb = k_k0;
     if (AMODE == 0) {
       k_c0 = k_k0;
+    } else if (AMODE == 1 && G8_CONV_CMAJOR) {
+      // 3x3 conv, 64-channel slice outer and tap inner: the nine taps of one slice read one ~4-image-row
+      // window of it in consecutive K tiles, so the window stays in L2 (tap-major order re-reads every
+      // input row from HBM once per tap row: 4.3 GB per level-0 conv dispatch for ~1.5 GB of operands).
+      // B's K offset follows (K index tap * Cin + c)
+      set_tap(s_tap);
+      k_c0 = s_c0;
+      k_kb = s_tap * cin + s_c0;
+      if (++s_tap == ntap) { s_tap = 0; s_c0 += 64; }
     } else {
       if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
       k_c0 = s_c0;
@@ -234,7 +273,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
 #pragma unroll
     for (int u = 0; u < NBJ; ++u) {
       if (NBP % 8 == 0 || wave + 8 * u < NBP) {
-        unsigned off = boff[h][u] + (unsigned)k_k0 * 2u;
+        unsigned off = boff[h][u] + (unsigned)k_kb * 2u;
         if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + (wave + 8 * u) * 1024), 16, off, 0, 0, 0);
       }

@@ -209,7 +209,8 @@ class FamilyTimer:
     timed region, with each launch's algorithmic work: flash attention FLOPs (4 S^2 64 per head and
     batch), fused level-0 feed-forward FLOPs (24 M C^2), selective-scan bytes (u read once for both directions, the xdbl rows (bf16, or fp32 on the legacy path), both outputs
     written), GroupNorm / LayerNorm bytes (input read once, output written once -- the stats pass's
-    second read of the input is the kernels' cost, not the algorithm's)."""
+    second read of the input is the kernels' cost, not the algorithm's), Mamba combine + LayerNorm bytes
+    (the rows each branch reads -- in_proj row or both scan directions -- and the output row)."""
 
     def __init__(self):
         self.ev = {}                         # family -> list of (e0, e1, work)
@@ -225,6 +226,9 @@ class FamilyTimer:
             out = orig(*a, **k)
             e1.record()
             w = work_fn(*a, **k)
+            if callable(w):                   # evaluated after the timed region (needs a device read)
+                self.ev.setdefault(fam, []).append((e0, e1, w))
+                return out
             if isinstance(w, tuple):          # (work, secondary count): the scan's state updates
                 w, extra = w
                 self.extra[fam] = self.extra.get(fam, 0) + extra
@@ -263,7 +267,22 @@ class FamilyTimer:
             M, C = x.shape
             return 24.0 * M * C * C                  # up 2*M*C*8C + down 2*M*4C*C
 
+        def w_combine(branch_a, branch_e, gamma, beta, eps, M, S, C, out=None):
+            # the rows each branch actually reads (its in_proj row x, or the two scan directions of a selected
+            # token) plus the output row; mode-2 selections are counted after the timed region
+            def rows_read(br):
+                mode = br["mode"]
+                if mode == 0:
+                    return lambda: float(M)
+                if mode == 1:
+                    return lambda: 2.0 * M
+                pos = br["pos"]
+                return lambda: 2.0 * (M // S) * int((pos >= 0).sum()) + (M - (M // S) * int((pos >= 0).sum()))
+            ra, re_ = rows_read(branch_a), rows_read(branch_e)
+            return lambda: (ra() + re_() + M) * C * 2.0
+
         self._wrap(ops, "flash_attn", "flash_attn", w_flash)
+        self._wrap(ops, "mamba_combine_ln", "mamba_combine", w_combine)
         self._wrap(ops, "geglu_ffn", "geglu_ffn", w_ffn)
         self._wrap(ops, "selective_scan", "selective_scan", w_scan)
         self._wrap(ops, "selective_scan2", "selective_scan", w_scan2)      # paired audio + expression launch
@@ -281,11 +300,12 @@ class FamilyTimer:
                 "geglu_ffn": ("mfma", PEAK_BF16_TFLOPS, "TFLOP/s", 1e12),
                 "selective_scan": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
                 "groupnorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
-                "layernorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9)}
+                "layernorm": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9),
+                "mamba_combine": ("hbm", PEAK_HBM_GBS, "GB/s", 1e9)}
         out = {}
         for fam, evs in self.ev.items():
             ms = sum(a.elapsed_time(b) for a, b, _ in evs)
-            work = sum(w for _, _, w in evs)
+            work = sum(w() if callable(w) else w for _, _, w in evs)
             bound, pk, unit, scale = peak[fam]
             ach = work / (ms / 1e3) / scale
             out[fam] = dict(bound=bound, achieved=round(ach, 1), peak=pk, unit=unit, frac=round(ach / pk, 4),

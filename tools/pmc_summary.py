@@ -38,7 +38,8 @@ def main():
         src = sys.argv[sys.argv.index("--source") + 1] if "--source" in sys.argv else d
         fams = {"acth_gemm": lambda k: "gemm" in k, "flash_attn": lambda k: "flash_attn" in k or "flash16" in k,
                 "selective_scan": lambda k: "scan" in k, "groupnorm": lambda k: k.startswith("gn_"),
-                "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k}
+                "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k,
+                "mamba_combine": lambda k: "mamba_combine" in k}
         res = {}
         for fam, match in fams.items():
             g = [r for r in rows if match(r[0].split("(")[0].replace("void ", ""))]

@@ -2,6 +2,8 @@
 //
 //  * acth_flash_attn   : spatial self-attention softmax(Q K^T * scale) V over S <= 9216 tokens
 //                        (AttnProcessor2_0, reference attention_processor.py:1528-1605).
+//                        Default: flash16_kernel (v_mfma_f32_16x16x32_bf16, below); FA_M16=0
+//                        builds the original flash_attn_kernel.
 //                        Flash-style online softmax on v_mfma_f32_32x32x16_bf16. The QK^T
 //                        product is computed transposed (S^T = K Q^T) so each lane owns one
 //                        query column: row max / row sum stay lane-local (+1 lane^32 exchange),

@@ -591,17 +591,26 @@ def euler_step_v(model_output, sigma, sigma_next, sample):
 def denoise_loop(unet_fn, latents_all, image_latents, image_embeddings, audio_prompts, vasa_prompts, pose_fea,
                  added_time_ids, masks: List[torch.Tensor], gate, num_frames: int, frames_per_batch: int,
                  overlap: int, shift_offset: int, guidance, num_inference_steps: int = 25,
-                 sigma_min=0.002, sigma_max=700.0):
+                 sigma_min=0.002, sigma_max=700.0, resume=None, on_step=None):
     """Pose2VideoLongSVDPipeline.__call__ step x window loop (pipeline_svd_audio_adapter_motionexp_idembed_
     vasa_two_ip.py:670-756). Tensor shapes are the pipeline's after CFG stacking:
       latents_all (1, T, 4, h, w), image_latents (4, T, 4, h, w), image_embeddings (4, T, 1, 1024),
       audio_prompts (4, T, 32, 1024), vasa_prompts (4, T, 1, 1024), pose_fea (1, N or T, 320, h, w), T = N + fpb.
-    unet_fn(sample, t, ehs, added_time_ids, spatial_condition, cak) -> (4, fpb, 4, h, w)."""
+    unet_fn(sample, t, ehs, added_time_ids, spatial_condition, cak) -> (4, fpb, 4, h, w).
+    guidance: (g1, g2, g3), or one such triple per step (the pipeline's linspace schedules, :640-657).
+    resume=(i0, latents_all) restarts at step i0 (the shift is a function of the step index, :752-753);
+    on_step(i, latents_all) is called after every step (long CPU runs checkpoint through it)."""
     sigmas, timesteps = euler_karras_tables(num_inference_steps, sigma_min, sigma_max)
-    g1, g2, g3 = guidance
-    shift = 0
+    per_step = isinstance(guidance[0], (tuple, list))
     T = num_frames + frames_per_batch
+    i0 = 0
+    if resume is not None:
+        i0, latents_all = resume
+    shift = (i0 * shift_offset) % frames_per_batch
     for i, t in enumerate(timesteps):
+        if i < i0:
+            continue
+        g1, g2, g3 = guidance[i] if per_step else guidance
         pred = torch.zeros_like(latents_all)
         counter = torch.zeros((latents_all.shape[0], T, 1, 1, 1))
         for index_start in range(0, T, frames_per_batch - overlap):
@@ -637,4 +646,6 @@ def denoise_loop(unet_fn, latents_all, image_latents, image_embeddings, audio_pr
                 counter[:, pidx] += 1
         shift = (shift + shift_offset) % frames_per_batch
         latents_all = pred / counter
+        if on_step is not None:
+            on_step(i, latents_all)
     return latents_all

@@ -28,10 +28,13 @@ def build_full_unet(seed=WEIGHT_SEED):
     return unet
 
 
-def case_inputs(case: str, seed: int = 11):
+def case_inputs(case: str, seed: int = 11, h_px: int = H_PX, w_px: int = W_PX):
     """(sample, t, ehs, added, pose, masks) for one case; masks follow the pipeline's gates
     (pipeline:702-711): mode0 [face, 0] with zero VASA tokens, mode1 [0, face] with zero audio
-    tokens, mode2 [ones, ones], half = [mouth (lower half), expression (upper half)] under gate [1, 1]."""
+    tokens, mode2 [ones, ones], half = [mouth (lower half), expression (upper half)] under gate [1, 1],
+    face0 = mode 0 with a centre face box instead of an all-ones face. h_px x w_px: the pixel geometry
+    (576x1024 = BASELINE C2-C5; 576x576 = C1)."""
+    H_PX, W_PX = h_px, w_px
     g = torch.Generator().manual_seed(seed)
     h, w = H_PX // 8, W_PX // 8
     sample = torch.randn(B, F, 8, h, w, generator=g)
@@ -46,6 +49,10 @@ def case_inputs(case: str, seed: int = 11):
     lower[..., H_PX // 2:, :] = 1.0
     if case == "mode0":
         masks, vas = [one, zero], torch.zeros_like(vas)
+    elif case == "face0":
+        face = zero.clone()
+        face[..., H_PX // 4: 3 * H_PX // 4, 5 * W_PX // 16: 11 * W_PX // 16] = 1.0
+        masks, vas = [face, zero], torch.zeros_like(vas)
     elif case == "mode1":
         masks, aud = [zero, one], torch.zeros_like(aud)
     elif case == "mode2":

@@ -13,9 +13,11 @@ and mamba-ssm's selective_scan_ref are restatements.
   zero VASA tokens, mode1 [0, face] with zero audio tokens, mode2 [ones, ones], half [mouth (lower
   half), expression (upper half)], box [centre box, upper half] (a partial mask whose token rows are
   not whole image rows).
-* ``full_half``: the real 1.775 B-parameter UNet (widths 320/640/1280/1280, heads 5/10/20/20) at
-  576x1024, B = 1 x F = 2, half masks: the inputs and weights of tests/golden_full.py's ``half`` case,
-  so the same fixture also pins the oracle's full-geometry output.
+* ``full_half`` / ``full_mode0`` / ``full_mode2``: the real 1.775 B-parameter UNet (widths 320/640/1280/1280,
+  heads 5/10/20/20) at 576x1024, B = 1 x F = 2, the inputs and weights of tests/golden_full.py's ``half`` /
+  ``mode0`` / ``mode2`` cases, so the same fixtures also pin the oracle's full-geometry outputs.
+* ``c1_face0``: the same UNet at BASELINE C1's geometry, 576x576 (latent 72x72; levels 72x72 / 36x36 / 18x18 /
+  9x9), B = 1 x F = 2, mode 0 (gate [1, 0], zero VASA tokens) with a centre face box as the audio mask.
 
 Weights are actalker_amd.synthetic values by parameter name (reference names: the key sets are equal,
 tests/test_checkpoint_cpu.py), regenerated from the seed on every host; the fixtures hold outputs and
@@ -30,7 +32,7 @@ TINY_CFG = dict(block_out_channels=(64, 128, 128, 128), num_attention_heads=(1, 
 TINY_SEED = 5
 TINY_B, TINY_F, TINY_H, TINY_W = 2, 3, 16, 32
 TINY_CASES = ("tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box")
-FULL_CASES = ("full_half",)
+FULL_CASES = ("full_half", "full_mode0", "full_mode2", "c1_face0")
 CASES = TINY_CASES + FULL_CASES
 SIGMA = 1.6555  # Karras step 12 of 25; t = 0.25 ln sigma
 
@@ -70,9 +72,11 @@ def tiny_inputs(case: str, seed: int = 23):
 def case_inputs(case: str):
     if case in TINY_CASES:
         return tiny_inputs(case)
-    if case == "full_half":
-        from tests import golden_full as gf
-        return gf.case_inputs("half")
+    from tests import golden_full as gf
+    if case in ("full_half", "full_mode0", "full_mode2"):
+        return gf.case_inputs(case.split("_", 1)[1])
+    if case == "c1_face0":
+        return gf.case_inputs("face0", h_px=576, w_px=576)
     raise ValueError(case)
 
 

@@ -78,7 +78,8 @@ def test_unet_full_geometry_matches_oracle(dev, full_unet, case):
     _log(f"unet_full_{case}", st)
     assert torch.isfinite(out).all()
     assert st["rel_l2"] < 2e-2, st
-    assert st["max_abs"] < 0.25 * max(1.0, st["ref_rms"]), st
+    # max |err| gate ~3x the measured 0.031-0.045 on outputs of rms ~0.55-0.62 (profiles/r3_final_parity.jsonl)
+    assert st["max_abs"] < 0.25 * st["ref_rms"], st
     if "bf16_rounding_rel_l2" in st:
         # stated tolerance: the HIP bf16 error stays within 1.5x of what bf16 rounding at op boundaries alone
         # costs (fp16 rounding costs ~8x less: 3 more mantissa bits)
@@ -175,6 +176,7 @@ def test_pipeline_25_steps_matches_oracle(dev, loop_unet, mode):
     _log(f"loop25_{mode}", st)
     assert torch.isfinite(got).all()
     assert st["rel_l2"] < 3e-2, st
+    assert st["max_abs"] < 0.25 * st["ref_rms"], st
 
 
 @pytest.mark.parametrize("mode", ["mode0", "mode2"])
@@ -205,10 +207,47 @@ def test_pipeline_25_steps_real_width_matches_oracle(dev, full_unet, mode):
     assert torch.isfinite(got).all()
     assert st["rel_l2"] < 5e-2, st
     assert st["rel_l2"] < 1.5 * st["bf16_rounding_rel_l2"], st
+    assert st["max_abs"] < 0.25 * st["ref_rms"], st
+
+
+def test_c1_loop_matches_cpu_oracle(dev, full_unet):
+    """BASELINE C1 end to end: mode 0, 14 frames, 25 steps, 576x576 (latent 72x72), fpb 14,
+    shift 7, the full-size UNet -- the HIP loop on exactly the workload tools/gen_golden_c1.py ran through the fp32
+    oracle on the CPU (tests/golden_c1.py). Stated tolerance: the bf16-rounding floor the real-width loop measures
+    (1.5-1.8e-2 after 25 steps, test above) with the same 1.5x factor when the bf16-rounded C1 loop is present,
+    else rel-L2 < 5e-2 (the absolute cap of the real-width loop test)."""
+    from actalker_amd import pipeline as pl
+    from tests import golden_c1 as gc
+    path = os.path.join(GOLD, "c1_loop25_mode0.safetensors")
+    if not os.path.exists(path):
+        pytest.skip("C1 oracle loop fixture not generated (tools/gen_golden_c1.py)")
+    g = load_file(path)
+    unet, wsum = full_unet
+    torch.testing.assert_close(wsum, g["weights_checksum"], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(gc.inputs_checksum(), g["inputs_checksum"], rtol=1e-6, atol=1e-6)
+    latents, imgl, ide, aud, vas, pose, added, masks = gc.loop_inputs()
+    T = gc.N + gc.FPB
+    backend = pl.HipBackend(unet, gc.H, gc.W, masks, gc.GATE, added, T, gc.FPB, imgl, ide, aud, vas, pose)
+    assert backend.branch_twins() == {3: 2}
+    lc = pl.LoopConfig(num_frames=gc.N, frames_per_batch=gc.FPB, overlap=gc.OVERLAP, shift_offset=gc.SHIFT,
+                       num_inference_steps=25, guidance=gc.GUIDANCE)
+    with torch.no_grad():
+        got = pl.denoise(backend, latents, lc)
+    want = g["latents"]
+    st = _stats(got, want)
+    tol = 5e-2
+    if "latents_bf16" in g:
+        st["bf16_rounding_rel_l2"] = ((g["latents_bf16"] - want).norm() / want.norm()).item()
+        tol = min(tol, 1.5 * st["bf16_rounding_rel_l2"])
+    _log("c1_loop25_mode0", st)
+    assert torch.isfinite(got).all()
+    assert st["rel_l2"] < tol, st
+    assert st["max_abs"] < 0.25 * st["ref_rms"], st
 
 
 # ------------------------------------------------------------------------------------------ reference run
-@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box", "full_half"])
+@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box", "full_half",
+                                  "full_mode0", "full_mode2", "c1_face0"])
 def test_unet_matches_reference_run(dev, request, case):
     """HIP UNet forward against the REFERENCE UNet package's own forward (v10:362-517 and everything under it,
     run unchanged on the CPU by tools/gen_golden_unet_ref.py; only the diffusers leaves and the scan math
@@ -233,4 +272,38 @@ def test_unet_matches_reference_run(dev, request, case):
     _log(f"unet_ref_{case}", st)
     assert torch.isfinite(out).all()
     assert st["rel_l2"] < 2e-2, st
-    assert st["max_abs"] < 0.25 * max(1.0, st["ref_rms"]), st
+    # ~3x the measured max |err| (0.032-0.045 at rms ~0.57-0.62, profiles/r3_final_parity.jsonl)
+    assert st["max_abs"] < 0.25 * st["ref_rms"], st
+
+
+# ------------------------------------------------------------------------------------------ reference sampler run
+@pytest.mark.parametrize("case", ["mode0", "mode1", "mode2"])
+def test_pipeline_call_matches_reference_pipeline_run(dev, case):
+    """The product Pose2VideoLongSVDPipeline.__call__ (actalker_amd/pipeline_svd.py: CFG stacking, add_noise,
+    masks / pose plumbing, per-step guidance, the HIP loop) against the REFERENCE pipeline's own __call__
+    (pipeline:351-773, run unchanged on the CPU by tools/gen_golden_pipeline_ref.py with the reference UNet
+    package at the same tiny widths and the reference scheduler mirror), 25 steps, output_type="latent", the
+    same deterministic VAE / ID-projection / pose-guider stand-ins (tests/golden_pipeline.py). Tolerance as the
+    tiny-topology loop test: rel-L2 < 3e-2 (bf16 UNet vs fp32)."""
+    from actalker_amd.pipeline_svd import Pose2VideoLongSVDPipeline
+    from tests import golden_pipeline as gp
+    from tests import golden_unet_ref as gu
+    path = os.path.join(GOLD, f"pipeline_ref_{case}.safetensors")
+    if not os.path.exists(path):
+        pytest.skip("reference pipeline fixture not generated (tools/gen_golden_pipeline_ref.py)")
+    g = load_file(path)
+    unet = gu.build_hip_unet("tiny_mode0")
+    sd = unet.state_dict()
+    torch.testing.assert_close(gf.checksum(*[sd[k] for k in sorted(sd)]), g["weights_checksum"], rtol=1e-6, atol=1e-6)
+    gate, overlap, shift = gp.CASES[case]
+    vae, idp, pg = gp.standins(gu.TINY_CFG["block_out_channels"][0])
+    pipe = Pose2VideoLongSVDPipeline(vae, unet, idp, pg).to(dev)
+    raw = gp.raw_inputs()
+    with torch.no_grad():
+        got = pipe(**raw, generator=torch.Generator().manual_seed(gp.GEN_SEED), output_type="latent",
+                   return_dict=False, overlap=overlap, shift_offset=shift, gate=gate, **gp.CALL)
+    st = _stats(got, g["latents"])
+    _log(f"pipeline_ref_{case}", st)
+    assert torch.isfinite(got).all()
+    assert st["rel_l2"] < 3e-2, st
+    assert st["max_abs"] < 0.25 * st["ref_rms"], st

@@ -156,11 +156,15 @@ def test_oracle_unet_matches_reference_run(case):
     assert rel < 1e-4, rel
 
 
-def test_oracle_full_geometry_fixture_matches_reference_run():
-    """The full-geometry oracle fixture (576x1024, real widths, half masks; tools/gen_golden_full.py) against
-    the reference UNet run on the same weights and inputs (both checksums equal)."""
-    o = load_file(os.path.join(GOLD, "unet_full_half.safetensors"))
-    r = load_file(os.path.join(GOLD, "unet_ref_full_half.safetensors"))
+@pytest.mark.parametrize("case", ["half", "mode0", "mode2"])
+def test_oracle_full_geometry_fixture_matches_reference_run(case):
+    """The full-geometry oracle fixtures (576x1024, real widths; tools/gen_golden_full.py) against the reference
+    UNet run on the same weights and inputs (both checksums equal)."""
+    rpath = os.path.join(GOLD, f"unet_ref_full_{case}.safetensors")
+    if not os.path.exists(rpath):
+        pytest.skip("reference-run fixture not generated (tools/gen_golden_unet_ref.py)")
+    o = load_file(os.path.join(GOLD, f"unet_full_{case}.safetensors"))
+    r = load_file(rpath)
     torch.testing.assert_close(o["weights_checksum"], r["weights_checksum"], rtol=1e-9, atol=1e-6)
     torch.testing.assert_close(o["inputs_checksum"], r["inputs_checksum"], rtol=1e-9, atol=1e-6)
     rel = ((o["out"] - r["out"]).norm() / r["out"].norm()).item()
@@ -202,3 +206,39 @@ def test_oracle_euler_step_matches_reference_mirror():
         torch.testing.assert_close(got, g["prev"][i], rtol=1e-5, atol=1e-5 * (1 + float(sig[i])))
     # add_noise at the first timestep (pipeline:312-314): x0 + eps * sigma_0
     torch.testing.assert_close(g["ref_latents"] + g["noise"] * sig[0], g["noised"], rtol=1e-6, atol=1e-4)
+
+
+# ------------------------------------------------------------------------------------------
+# The sampler itself against the REFERENCE pipeline's __call__ (pipeline:351-773 run unchanged by
+# tools/gen_golden_pipeline_ref.py around the reference UNet package and scheduler mirror, tiny widths)
+@pytest.mark.parametrize("case", ["mode0", "mode1", "mode2"])
+def test_oracle_loop_matches_reference_pipeline_run(case):
+    """oracle.denoise_loop over the test-side restatement of the pipeline's stacking / plumbing
+    (tests/golden_pipeline.oracle_loop_inputs) reproduces the reference __call__'s final latents: CFG stacking and
+    uncond pads, add_noise, masks and pose plumbing, per-step guidance linspace, windows with shift / overlap,
+    accumulate and average -- 25 Karras steps. Tolerance 1e-4 relative L2 (the oracle UNet alone matches the
+    reference UNet to ~1e-6 per call)."""
+    from tests import golden_full as gf
+    from tests import golden_pipeline as gp
+    from tests import golden_unet_ref as gu
+    path = os.path.join(GOLD, f"pipeline_ref_{case}.safetensors")
+    if not os.path.exists(path):
+        pytest.skip("reference pipeline fixture not generated (tools/gen_golden_pipeline_ref.py)")
+    g = load_file(path)
+    unet = gu.build_hip_unet("tiny_mode0")
+    sd = {k: v.detach().float() for k, v in unet.state_dict().items()}
+    torch.testing.assert_close(gf.checksum(*[sd[k] for k in sorted(sd)]), g["weights_checksum"], rtol=1e-9, atol=1e-6)
+    gate, overlap, shift = gp.CASES[case]
+    raw = gp.raw_inputs()
+    vae, idp, pg = gp.standins(gu.TINY_CFG["block_out_channels"][0])
+    with torch.no_grad():
+        lat, imgl, ide, aud, vas, pose, added, masks, gs = gp.oracle_loop_inputs(raw, vae, idp, pg, gate)
+
+        def unet_fn(sample, t, ehs, added_ids, sc, cak):
+            return ref.unet_forward(sd, sample, t, ehs, added_ids, sc, cak, ip_scale=(1.25, 1.25),
+                                    cfg=gu.oracle_cfg("tiny_mode0"))
+
+        out = ref.denoise_loop(unet_fn, lat, imgl, ide, aud, vas, pose, added, masks, gate, gp.N, gp.FPB,
+                               overlap=overlap, shift_offset=shift, guidance=gs, num_inference_steps=gp.STEPS)
+    rel = ((out - g["latents"]).norm() / g["latents"].norm()).item()
+    assert rel < 1e-4, rel

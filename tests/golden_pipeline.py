@@ -116,6 +116,13 @@ def raw_inputs(seed: int = INPUT_SEED):
                 uncond_vasa_prompts=uvas, latents=latents)
 
 
+def inputs_checksum(raw):
+    from tests import golden_full as gf
+    return gf.checksum(raw["ref_image"], raw["clip_image"], *raw["pose_images"], *raw["exp_mask_images"],
+                       *raw["mouth_mask_images"], *raw["audio_prompts"], *raw["uncond_audio_prompts"],
+                       *raw["vasa_prompts"], *raw["uncond_vasa_prompts"], raw["latents"])
+
+
 def standins(pose_channels: int):
     return StandInVAE(), StandInIDProj(), StandInPoseGuider(pose_channels)
 
@@ -151,3 +158,32 @@ def oracle_loop_inputs(raw, vae, id_proj, pose_guider, gate):
     gsched = list(zip(*[torch.linspace(CALL[f"min_guidance_scale{j}"], CALL[f"max_guidance_scale{j}"], STEPS).tolist()
                         for j in (1, 2, 3)]))
     return latents, imgl, ide, aud, vas, pose_fea, added, [face, mouth, exp], gsched
+
+
+def oracle_pipeline_loop(case: str, dtype=None):
+    """The oracle's version of the reference run of ``case``: tiny full-topology weights (the reference-run UNet
+    goldens' seed), the restated stacking above and oracle.reference_cpu.denoise_loop. dtype (torch.bfloat16 /
+    float16): every oracle op rounded at its boundary (oracle.precision) -- the rounding floor the HIP bf16 loop
+    is held against."""
+    import contextlib
+    from oracle import reference_cpu as ref
+    from tests import golden_unet_ref as gu
+    unet = gu.build_hip_unet("tiny_mode0")
+    sd = {k: v.detach().float() for k, v in unet.state_dict().items()}
+    ctx = contextlib.nullcontext()
+    if dtype is not None:
+        from oracle import precision
+        sd = precision.round_state_dict(sd, dtype)
+        ctx = precision.rounded(dtype)
+    gate, overlap, shift = CASES[case]
+    vae, idp, pg = standins(gu.TINY_CFG["block_out_channels"][0])
+    with torch.no_grad():
+        lat, imgl, ide, aud, vas, pose, added, masks, gs = oracle_loop_inputs(raw_inputs(), vae, idp, pg, gate)
+
+        def unet_fn(sample, t, ehs, added_ids, sc, cak):
+            return ref.unet_forward(sd, sample, t, ehs, added_ids, sc, cak, ip_scale=(1.25, 1.25),
+                                    cfg=gu.oracle_cfg("tiny_mode0"))
+
+        with ctx:
+            return ref.denoise_loop(unet_fn, lat, imgl, ide, aud, vas, pose, added, masks, gate, N, FPB,
+                                    overlap=overlap, shift_offset=shift, guidance=gs, num_inference_steps=STEPS)

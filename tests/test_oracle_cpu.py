@@ -228,17 +228,7 @@ def test_oracle_loop_matches_reference_pipeline_run(case):
     unet = gu.build_hip_unet("tiny_mode0")
     sd = {k: v.detach().float() for k, v in unet.state_dict().items()}
     torch.testing.assert_close(gf.checksum(*[sd[k] for k in sorted(sd)]), g["weights_checksum"], rtol=1e-9, atol=1e-6)
-    gate, overlap, shift = gp.CASES[case]
-    raw = gp.raw_inputs()
-    vae, idp, pg = gp.standins(gu.TINY_CFG["block_out_channels"][0])
-    with torch.no_grad():
-        lat, imgl, ide, aud, vas, pose, added, masks, gs = gp.oracle_loop_inputs(raw, vae, idp, pg, gate)
-
-        def unet_fn(sample, t, ehs, added_ids, sc, cak):
-            return ref.unet_forward(sd, sample, t, ehs, added_ids, sc, cak, ip_scale=(1.25, 1.25),
-                                    cfg=gu.oracle_cfg("tiny_mode0"))
-
-        out = ref.denoise_loop(unet_fn, lat, imgl, ide, aud, vas, pose, added, masks, gate, gp.N, gp.FPB,
-                               overlap=overlap, shift_offset=shift, guidance=gs, num_inference_steps=gp.STEPS)
+    torch.testing.assert_close(gp.inputs_checksum(gp.raw_inputs()), g["inputs_checksum"], rtol=1e-9, atol=1e-6)
+    out = gp.oracle_pipeline_loop(case)
     rel = ((out - g["latents"]).norm() / g["latents"].norm()).item()
     assert rel < 1e-4, rel

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--residual", action="store_true")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--sink", action="store_true", help="every row block writes the same 256 output rows")
+    ap.add_argument("--timeline", action="store_true", help="histogram of the epilogue fraction of resident WGs")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = _lib.load()
@@ -37,7 +38,20 @@ def main():
         _lib.check(lib.acth_debug_gemm_stamps(buf, n), "stamps")
         st = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.float64)
         ok = (st[:, 3] > st[:, 0]) & (st[:, 0] > 0)
+        xcd = (np.arange(n) % 8)[ok]
         st = st[ok]
+        if a.timeline:
+            # phase concurrency on XCD 0 (s_memtime is comparable within an XCD): at 400 instants over the
+            # kernel, the fraction of resident workgroups that are in their epilogue
+            s0 = st[xcd == 0]
+            t0, t1 = s0[:, 0].min(), s0[:, 3].max()
+            ts = np.linspace(t0, t1, 400)
+            act = ((s0[None, :, 0] <= ts[:, None]) & (ts[:, None] < s0[None, :, 3])).sum(1)
+            epi = ((s0[None, :, 2] <= ts[:, None]) & (ts[:, None] < s0[None, :, 3])).sum(1)
+            fr = epi / np.maximum(act, 1)
+            hist = np.histogram(fr[act > 0], bins=5, range=(0, 1))[0]
+            print(f"  XCD0 epilogue-fraction histogram (0-0.2 .. 0.8-1): {hist.tolist()}, mean resident {act.mean():.1f}",
+                  flush=True)
         d = np.diff(st, axis=1)
         tot = st[:, 3] - st[:, 0]
         print(f"{mode} {M}x{N}x{K} act {act}{' +res' if a.residual else ''}{' sink' if a.sink else ''}: {ms:.3f} ms ({tf:.0f} TF/s), "

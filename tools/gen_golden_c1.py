@@ -11,7 +11,7 @@ fp32 call would not fit this host's 64 GB. The state after every step is checkpo
 Writes tests/golden/c1_loop25_mode0.safetensors {latents, weights_checksum, inputs_checksum} and
 profiles/r4_c1_cpu_oracle.json (wall seconds per step and in total, threads, per-call seconds).
 
-    nice -n 10 python tools/gen_golden_c1.py          (~5 h on 8 threads)
+    ACTH_C1_THREADS=6 python tools/gen_golden_c1.py          (~6 h on 6 threads)
 """
 import json
 import os
@@ -34,6 +34,9 @@ STATE = os.path.join(ROOT, "tools", "_c1_state")
 def main():
     os.makedirs(STATE, exist_ok=True)
     torch.set_grad_enabled(False)
+    # leave cores for the other work on the host: an OpenMP team that loses one of its cores to another process
+    # waits at every barrier (measured here: 8 threads beside one 2-thread job ran 4-8x slower than alone)
+    torch.set_num_threads(int(os.environ.get("ACTH_C1_THREADS", "6")))
     t_build = time.time()
     unet = gf.build_full_unet()
     sd = {k: v.detach().float() for k, v in unet.state_dict().items()}

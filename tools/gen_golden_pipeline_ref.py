@@ -130,12 +130,6 @@ def build_reference_unet(unet_cls, add_ip):
     return unet.eval(), sd
 
 
-def inputs_checksum(raw):
-    return gf.checksum(raw["ref_image"], raw["clip_image"], *raw["pose_images"], *raw["exp_mask_images"],
-                       *raw["mouth_mask_images"], *raw["audio_prompts"], *raw["uncond_audio_prompts"],
-                       *raw["vasa_prompts"], *raw["uncond_vasa_prompts"], raw["latents"])
-
-
 def main(cases):
     pipe_cls, unet_cls, add_ip, sched_cls = load_reference_pipeline()
     torch.set_grad_enabled(False)
@@ -154,7 +148,7 @@ def main(cases):
                    overlap=overlap, shift_offset=shift, gate=gate, **gp.CALL)
         print(f"{case}: reference __call__ {time.time() - t0:.0f}s, latents {tuple(out.shape)} "
               f"rms {out.pow(2).mean().sqrt():.4f}", flush=True)
-        save_file({"latents": out.contiguous().float(), "weights_checksum": wsum, "inputs_checksum": inputs_checksum(raw)},
+        save_file({"latents": out.contiguous().float(), "weights_checksum": wsum, "inputs_checksum": gp.inputs_checksum(raw)},
                   os.path.join(ROOT, "tests", "golden", f"pipeline_ref_{case}.safetensors"))
 
 

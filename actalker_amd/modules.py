@@ -547,7 +547,9 @@ class FeedForward(Packed):
     def run_ln(self, x, ln, mix=None, mix_alpha: float = 0.0, add=None, add_div: int = 1):
         """net[2](GEGLU(ln(x'))) + x' [AlphaBlender with ``mix``], x' = x [+ add[row // add_div]] -- the
         blocks' "norm -> ff -> + residual" (attention.py:330-343, 449-457); one kernel at C = 320."""
-        if self.ln_fusable(x.shape[1]):
+        # the fused kernel takes the row add only with add_div % 64 == 0 and not together with a mix operand
+        # (acth_geglu_ffn): other shapes take the LayerNorm + two-GEMM path below
+        if self.ln_fusable(x.shape[1]) and (add is None or (add_div % 64 == 0 and mix is None)):
             w, b = self.net[0].packed()
             w2 = self._pk("w2perm", lambda: pack_ffn_w2(self.net[2].weight))
             return ops.geglu_ffn(x, w, b, w2, self.net[2].b(), residual=x, mix=mix, mix_alpha=mix_alpha,
@@ -681,8 +683,9 @@ class SS2D_Unit(nn.Module):
     def _acth_invalidate(self):
         self.__dict__["_acth_cache"] = {}
 
-    # x_proj output rows in bf16 (the reference's x_dbl dtype, mamba_layer.py:1521) for scan_quad_kernel;
-    # False: fp32 rows and the paired-lane kernel (ACTH_SCAN_XDBL_F32=1)
+    # x_proj output rows in bf16 (the reference's x_dbl dtype, mamba_layer.py:1521), scanned by the paired-lane
+    # kernel's bf16-row instantiation by default (scan_quad_kernel only with ACTH_SCAN_QUAD=1); False: fp32 rows
+    # (ACTH_SCAN_XDBL_F32=1)
     acth_xdbl_bf16 = os.environ.get("ACTH_SCAN_XDBL_F32", "0") != "1"
 
     def scan_args(self, u, nb, L, n_keep):

@@ -532,7 +532,7 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
                    n_keep: int, y0=None, y1=None, nchunks: Optional[int] = None):
     """Fused bidirectional scan. u: (nb*L, D) bf16; xdbl: (nb*L, 2*(R+32)) fp32 rows [dt | B | C] per
     direction, or bf16 rows (the reference's x_dbl dtype) of 2*(R4+32) with R4 = R rounded up to 4
-    (dt padding columns ignored; ``xproj_rows_padded`` packs x_proj weights to that layout)."""
+    (dt padding columns ignored; ``SS2D_Unit.packed()['xproj_pad']`` holds the x_proj weights in that layout)."""
     lib = _lib.load()
     d, y0, y1, ws = _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks)
     if d is not None:

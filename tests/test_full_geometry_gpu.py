@@ -283,8 +283,10 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case):
     masks / pose plumbing, per-step guidance, the HIP loop) against the REFERENCE pipeline's own __call__
     (pipeline:351-773, run unchanged on the CPU by tools/gen_golden_pipeline_ref.py with the reference UNet
     package at the same tiny widths and the reference scheduler mirror), 25 steps, output_type="latent", the
-    same deterministic VAE / ID-projection / pose-guider stand-ins (tests/golden_pipeline.py). Tolerance as the
-    tiny-topology loop test: rel-L2 < 3e-2 (bf16 UNet vs fp32)."""
+    same deterministic VAE / ID-projection / pose-guider stand-ins (tests/golden_pipeline.py). Stated tolerance:
+    within 1.5x of the deviation the bf16-rounded oracle version of the same run accumulates over the 25 steps
+    (tools/gen_golden_pipeline_floor.py; the per-step guidance here reaches 7.5, so the rounding floor is higher
+    than the constant-guidance loop's), and below 5e-2."""
     from actalker_amd.pipeline_svd import Pose2VideoLongSVDPipeline
     from tests import golden_pipeline as gp
     from tests import golden_unet_ref as gu
@@ -303,7 +305,13 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case):
         got = pipe(**raw, generator=torch.Generator().manual_seed(gp.GEN_SEED), output_type="latent",
                    return_dict=False, overlap=overlap, shift_offset=shift, gate=gate, **gp.CALL)
     st = _stats(got, g["latents"])
+    tol = 3e-2
+    fpath = os.path.join(GOLD, f"pipeline_floor_{case}.safetensors")
+    if os.path.exists(fpath):
+        fl = load_file(fpath)
+        st["bf16_rounding_rel_l2"] = ((fl["latents_bf16"] - fl["latents"]).norm() / fl["latents"].norm()).item()
+        tol = min(5e-2, 1.5 * st["bf16_rounding_rel_l2"])
     _log(f"pipeline_ref_{case}", st)
     assert torch.isfinite(got).all()
-    assert st["rel_l2"] < 3e-2, st
+    assert st["rel_l2"] < tol, st
     assert st["max_abs"] < 0.25 * st["ref_rms"], st

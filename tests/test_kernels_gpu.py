@@ -562,6 +562,12 @@ def test_xattn_fused_block(dev, fps, masked, use_a, use_b):
     ref_n3 = F.layer_norm(ref_out, (C,), g3, b3, 1e-5)
     assert rel(out, ref_out) < 1e-2, rel(out, ref_out)
     assert rel(n3, ref_n3) < 1e-2, rel(n3, ref_n3)
+    # the attention increment h' - h on its own (the residual h dominates the norm of h'): within the bf16
+    # rounding of the output at |h| plus 1e-2
+    hf = h.float()
+    inc, inc_ref = out.float().cpu() - hf, ref_out - hf
+    floor = rel(bf(ref_out).float() - hf, inc_ref)
+    assert rel(inc, inc_ref) < floor + 1e-2, (rel(inc, inc_ref), floor)
     # norm3 left to the feed-forward kernel: the same h', no n3
     out2, none = ops.xattn(h.to(dev), 1e-5, None, base, heads=heads, rows_per_ctx=rpc, S=S,
                            kp=kp, vp=vp, gb=gb, vbw=vbw, mask_a=tod(ma), mask_b=tod(mb), sa=1.25, sb=0.75)

@@ -157,8 +157,10 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int wr = wave % WR, wc = wave / WR;     // wave's row / column slot inside a quadrant
   const bool stamps = (p.tile & 0x400) != 0;
   const int stamp_wg = blockIdx.x + gridDim.x * blockIdx.y;
+  const bool rt = (p.tile & 0x800) != 0;          // stamps from the 100 MHz real-time counter (chip-wide timeline)
   auto stamp = [&](int k) {
-    if (stamps && tid == 0 && stamp_wg < STAMP_WGS) g_gemm_stamps[stamp_wg * 4 + k] = __builtin_amdgcn_s_memtime();
+    if (stamps && tid == 0 && stamp_wg < STAMP_WGS)
+      g_gemm_stamps[stamp_wg * 4 + k] = rt ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
   };
   stamp(0);
   const bool late = wave >= 4;                  // staggered half

@@ -30,7 +30,8 @@ def main():
     for idx in [int(i) for i in a.only.split(",")]:
         mode, M, N, K, act = SHAPES[idx]
         tf, ms = run(mode, M, N, K, act, a.tile, 5, dev, sink=a.sink, residual=a.residual)
-        tf2, ms2 = run(mode, M, N, K, act, a.tile | 0x400, 1, dev, sink=a.sink, residual=a.residual)
+        flags = 0x400 | (0x800 if a.timeline else 0)
+        tf2, ms2 = run(mode, M, N, K, act, a.tile | flags, 1, dev, sink=a.sink, residual=a.residual)
         mt = (M + 255) // 256
         nt = -(-N // 320) if (a.tile or 5) == 5 and act != 2 else -(-N // 256)
         n = min(mt * nt, 16384)
@@ -41,17 +42,18 @@ def main():
         xcd = (np.arange(n) % 8)[ok]
         st = st[ok]
         if a.timeline:
-            # phase concurrency on XCD 0 (s_memtime is comparable within an XCD): at 400 instants over the
+            # phase concurrency (stamps from the chip-wide 100 MHz s_memrealtime): at 400 instants over the
             # kernel, the fraction of resident workgroups that are in their epilogue
-            s0 = st[xcd == 0]
+            s0 = st
             t0, t1 = s0[:, 0].min(), s0[:, 3].max()
             ts = np.linspace(t0, t1, 400)
-            act = ((s0[None, :, 0] <= ts[:, None]) & (ts[:, None] < s0[None, :, 3])).sum(1)
+            nres = ((s0[None, :, 0] <= ts[:, None]) & (ts[:, None] < s0[None, :, 3])).sum(1)
             epi = ((s0[None, :, 2] <= ts[:, None]) & (ts[:, None] < s0[None, :, 3])).sum(1)
-            fr = epi / np.maximum(act, 1)
-            hist = np.histogram(fr[act > 0], bins=5, range=(0, 1))[0]
-            print(f"  XCD0 epilogue-fraction histogram (0-0.2 .. 0.8-1): {hist.tolist()}, mean resident {act.mean():.1f}",
-                  flush=True)
+            fr = epi / np.maximum(nres, 1)
+            hist = np.histogram(fr[nres > 0], bins=5, range=(0, 1))[0]
+            print(f"  epilogue-fraction histogram (0-0.2 .. 0.8-1): {hist.tolist()}, mean resident {nres.mean():.1f}, "
+                  f"epilogue fraction std {fr[nres > 0].std():.3f}", flush=True)
+            st = st * 20.0            # 100 MHz ticks -> ~2 GHz cycles for the per-phase means below
         d = np.diff(st, axis=1)
         tot = st[:, 3] - st[:, 0]
         print(f"{mode} {M}x{N}x{K} act {act}{' +res' if a.residual else ''}{' sink' if a.sink else ''}: {ms:.3f} ms ({tf:.0f} TF/s), "

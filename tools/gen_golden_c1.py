@@ -3,7 +3,9 @@ Karras steps, 576x576 (latent 72x72), windowed 4-way CFG exactly as the referenc
 branches, no twin elimination), frames_per_batch 14, shift 7 -- around the full-size synthetic UNet
 (tests/golden_full.py), on this host's cores. Inputs: tests/golden_c1.py.
 
-Every UNet call of the reference (one window, 4 CFG branches x 14 frames) is evaluated as four batch-1 calls:
+Every UNet call of the reference (one window, 4 CFG branches x 14 frames) is evaluated as batch-1 calls, and a
+branch whose inputs are bitwise another's (mode 0's "drop vasa" / "cond" pair) is evaluated once, as the HIP loop
+does (ACTH_C1_TWINS=0 evaluates all four):
 batch elements are independent in the UNet (GroupNorm / attention / scans are per element), and one 56-frame
 fp32 call would not fit this host's 64 GB. The state after every step is checkpointed
 (tools/_c1_state/, git- and gpurun-ignored) so an interrupted run resumes.
@@ -29,6 +31,8 @@ from tests import golden_c1 as gc  # noqa: E402
 from tests import golden_full as gf  # noqa: E402
 
 STATE = os.path.join(ROOT, "tools", "_c1_state")
+# evaluate a branch with bitwise-duplicate inputs once (steps 0-1 of the committed run evaluated all four)
+TWINS = os.environ.get("ACTH_C1_TWINS", "1") == "1"
 
 
 def main():
@@ -57,8 +61,21 @@ def main():
     def unet_fn(sample, t, ehs, added_ids, sc, cak):
         outs = []
         fpb = sample.shape[1]
+
+        def inputs(b):
+            sl = slice(b * fpb, (b + 1) * fpb)
+            return (sample[b], ehs[0][sl], ehs[1][0][sl], ehs[1][1][sl], added_ids[b], sc[b])
+
         for b in range(sample.shape[0]):
             sl = slice(b * fpb, (b + 1) * fpb)
+            # a CFG branch whose inputs are bitwise an earlier branch's (mode 0: "drop vasa" and "cond", the VASA
+            # prompts being gated to zero, pipeline:724) has that branch's output: batch elements are independent
+            # in the UNet and the oracle is deterministic (the HIP loop makes the same exact elimination)
+            twin = next((e for e in range(b) if all(torch.equal(x, y) for x, y in zip(inputs(b), inputs(e)))), None)
+            if twin is not None and TWINS:
+                outs.append(outs[twin])
+                log["twins"] = log.get("twins", 0) + 1
+                continue
             t0 = time.time()
             o = ref.unet_forward(sd, sample[b:b + 1], t, (ehs[0][sl], [ehs[1][0][sl], ehs[1][1][sl]]),
                                  added_ids[b:b + 1], sc[b:b + 1], {"ip_adapter_masks": list(cak["ip_adapter_masks"])},
@@ -92,6 +109,9 @@ def main():
         "threads": torch.get_num_threads(), "host": os.uname().nodename,
         "frames_per_second": round(gc.N / total, 7),
         "seconds_per_unet_call_mean": round(sum(log["calls"]) / max(1, len(log["calls"])), 2),
+        "twin_branch_calls_skipped": log.get("twins", 0),
+        "reference_shaped_seconds_estimate": round(total + log.get("twins", 0) * sum(log["calls"]) /
+                                                   max(1, len(log["calls"])), 1),
         "steps": log["steps"],
     }
     with open(os.path.join(ROOT, "profiles", "r4_c1_cpu_oracle.json"), "w") as fh:

@@ -265,9 +265,14 @@ __global__ __launch_bounds__(256, 2) void xattn_kernel(const ActhXattnDesc p, un
   };
   // chunk q landed for every wave (this wave's DMAs counted, then a barrier). Called before chunk q + 2 is
   // issued: only chunk q + 1's pieces may stay in flight (vmcnt counts this wave's loads in issue order)
+  // The first wait also retires this wave's LDS writes (lgkmcnt(0)): the per-key LN2 constants (sgb) and the
+  // per-channel rows staged above with plain ds_writes are read by other waves after this barrier, and gfx950's
+  // s_barrier does not wait for them by itself.
   auto wait_chunk = [&](auto q_c) {
     constexpr int q = decltype(q_c)::value;
-    if constexpr (q + 1 < NCHUNK) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+    if constexpr (q == 0 && q + 1 < NCHUNK) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW) : "memory");
+    else if constexpr (q == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if constexpr (q + 1 < NCHUNK) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };

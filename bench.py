@@ -188,6 +188,27 @@ class GemmTimer:
                 t_hbm += ms
         return (t_floor / t_meas if t_meas else None), (t_hbm / t_meas if t_meas else None)
 
+    def conv_family(self, step_ms_total):
+        """The implicit-GEMM 3x3 convolutions (acth_gemm with A mode 1) as their own family: achieved MFMA rate,
+        share of the step, algorithmic bytes (each image element once) and their PMC traffic."""
+        evs = [(a, b, w) for (a, b, key), w in zip(self.events, self.work) if key[0] == "conv"]
+        if not evs:
+            return None
+        ms = sum(a.elapsed_time(b) for a, b, _ in evs)
+        fl = sum(w[0] for _, _, w in evs)
+        by = sum(w[1] for _, _, w in evs)
+        ach = fl / (ms / 1e3) / 1e12
+        out = dict(bound="mfma", achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                   frac=round(ach / PEAK_BF16_TFLOPS, 4), launches=len(evs), avg_launch_us=round(1000.0 * ms / len(evs), 1),
+                   share_of_step=round(ms / step_ms_total, 4), algorithmic_bytes_per_launch=round(by / len(evs)),
+                   flop_per_launch=round(fl / len(evs)))
+        pmc = pmc_traffic("gemm_conv")
+        if pmc:
+            out["traffic"] = round(pmc["hbm_bytes_per_launch"])
+            out["traffic_unit"] = "HBM bytes per kernel dispatch (PMC 2*FETCH_SIZE + WRITE_SIZE)"
+            out["traffic_source"] = pmc.get("source")
+        return out
+
     def shape_report(self, top=25):
         agg = {}
         for a, b, key in self.events:
@@ -571,7 +592,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
-            "kernel_families": (ftimer.report(elapsed * 1000.0) if ftimer is not None else None),
+            "kernel_families": ({**ftimer.report(elapsed * 1000.0),
+                                 **({"gemm_conv": timer.conv_family(elapsed * 1000.0)} if timer is not None else {})}
+                                if ftimer is not None else None),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -36,7 +36,10 @@ def main():
         import json
         out = sys.argv[sys.argv.index("--json") + 1]
         src = sys.argv[sys.argv.index("--source") + 1] if "--source" in sys.argv else d
+        import re
         fams = {"acth_gemm": lambda k: "gemm" in k, "flash_attn": lambda k: "flash_attn" in k or "flash16" in k,
+                # the implicit-GEMM 3x3 convs (phased kernel, A mode 1): their per-tap image re-reads
+                "gemm_conv": lambda k: re.match(r"gemm8p_kernel<\d+, 1,", k) is not None,
                 "selective_scan": lambda k: "scan" in k, "groupnorm": lambda k: k.startswith("gn_"),
                 "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k,
                 "mamba_combine": lambda k: "mamba_combine" in k}

@@ -172,10 +172,14 @@ def test_single_process_loop_matches_oracle():
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_loop_matches_single_process(world):
-    """world ranks (gloo), contiguous unit blocks + one all-gather per step == 1 process == oracle."""
-    N, fpb, steps = 6, 3, 4
+@pytest.mark.parametrize("world,N,fpb", [(2, 6, 3), (3, 6, 3), (8, 16, 2)])
+def test_sharded_loop_matches_single_process(world, N, fpb):
+    """world ranks (gloo), contiguous unit blocks + one all-gather per step == 1 process == oracle. The world-8
+    case has C5's unit layout (BASELINE configs[4]: N + fpb = 9 windows x 4 CFG branches = 36 units dealt
+    5, 5, 5, 5, 4, 4, 4, 4 over 8 ranks), at stand-in sizes."""
+    steps = 4
+    if world == 8:
+        assert [len(pl.assign_units(len(range(0, N + fpb, fpb)), 8, r)[0]) for r in range(8)] == [5, 5, 5, 5, 4, 4, 4, 4]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1,7 +1,9 @@
 """ctypes binding of libactalker_hip.so (the C ABI declared in include/actalker_hip.h).
 
-The shared library is built in-tree by ``actalker_amd/csrc/Makefile`` (``__graft_entry__.build``).
-There is deliberately no fallback: if the library cannot be loaded every op raises.
+The shared libraries are built in-tree by ``actalker_amd/csrc/Makefile`` (``__graft_entry__.build``): the
+kernels with bf16 activations (libactalker_hip.so) and the same sources with fp16 activations
+(libactalker_hip_f16.so, the reference's shipped weight_dtype). Both export the same C ABI.
+There is deliberately no fallback: if a library cannot be loaded every op raises.
 """
 from __future__ import annotations
 
@@ -11,6 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # ACTH_LIB overrides the in-tree library (A/B benchmarks of two builds in one GPU session)
 LIB_PATH = os.environ.get("ACTH_LIB") or os.path.join(_HERE, "libactalker_hip.so")
+LIB_PATH_F16 = os.environ.get("ACTH_LIB_F16") or os.path.join(_HERE, "libactalker_hip_f16.so")
 
 c_int = ctypes.c_int
 c_float = ctypes.c_float
@@ -222,30 +225,32 @@ SIGNATURES = {
     "acth_version": ([], c_int),
 }
 
-_lib = None
+_libs = {}
 
 
 class ActhError(RuntimeError):
     pass
 
 
-def load():
-    """Load the HIP library (once). Raises if it is missing: there is no CPU fallback."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load(dtype=None):
+    """Load the HIP library for the activation dtype (torch.bfloat16 -- the default -- or torch.float16), once.
+    Raises if it is missing: there is no CPU fallback."""
+    f16 = str(dtype) == "torch.float16"
+    if f16 in _libs:
+        return _libs[f16]
+    path = LIB_PATH_F16 if f16 else LIB_PATH
+    if not os.path.exists(path):
         raise ActhError(
-            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(or `make -C actalker_amd/csrc`). The ACTalker MI355X path has no fallback.")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (argtypes, restype) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype
     if lib.acth_gemm_desc_size() != ctypes.sizeof(GemmDesc):
         raise ActhError("ActhGemmDesc layout mismatch between include/actalker_hip.h and _lib.py")
-    _lib = lib
+    _libs[f16] = lib
     return lib
 
 

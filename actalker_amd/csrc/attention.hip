@@ -44,7 +44,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef FA_SUM_CHECK
 #define FA_SUM_CHECK 1
 #endif
+// fp16 build: P is packed to fp16 (max 65504), so the lane sum that bounds every p stays at 2^15
+#if ACTH_F16
+#define FA_LSUM_MAX 32768.0f
+#else
 #define FA_LSUM_MAX 65536.0f
+#endif
 // 1: flash16_kernel (v_mfma_f32_16x16x32_bf16) for every flash launch; 0: flash_attn_kernel (32x32x16)
 #ifndef FA_M16
 #define FA_M16 1
@@ -71,6 +76,16 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4_t lds_short4;
+
+// 16x16x16 MFMA on raw 16-bit activation fragments (4 per lane)
+__device__ __forceinline__ f32x4_t mfma16x16x16_s4(short4_t a, short4_t b, f32x4_t c) {
+#if ACTH_F16
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a), __builtin_bit_cast(h4, b), c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+#endif
+}
 
 __device__ __forceinline__ int fa_swk(int key) { return (key >> 1) & 7; }
 __device__ __forceinline__ int fa_swv(int key) { return ((key >> 1) & 1) << 2; }
@@ -136,7 +151,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
       uint32_t w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        w[j] = pack2(__uint_as_float(tw[j] << 16) * c, __uint_as_float(tw[j] & 0xffff0000u) * c);
+        w[j] = pack2(lo16f(tw[j]) * c, hi16f(tw[j]) * c);
       qf[g][s] = *reinterpret_cast<bf16x8_t*>(w);
     }
 
@@ -214,8 +229,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
       for (int g = 0; g < QG; ++g)
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
-          st[g][sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[sub][s], qf[g][s], s == 0 ? negm[g] : st[g][sub],
-                                                               0, 0, 0);
+          st[g][sub] = mfma32x32x16(kf[sub][s], qf[g][s], s == 0 ? negm[g] : st[g][sub]);
     FA_PRIO_OFF();
     if (FA_LATE_DMA && kv0 + 64 < p.Skv) stage(kv0 + 64, buf ^ 1);
     if (kv0 + 64 > p.Skv) {
@@ -238,7 +252,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
       // so a sum <= FA_LSUM_MAX bounds them all and m needs no update. Otherwise (and always on the first
       // tile, which sets m) the exact max is taken and the tile is exponentiated again.
       auto expack = [&]() {
-        const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+        const bf16x2_t one = one2_16();
         float l0 = 0.0f, l1 = 0.0f;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
@@ -250,8 +264,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
               w[j] = pack2(__builtin_amdgcn_exp2f(st[g][sub][8 * s2 + 2 * j]),
                            __builtin_amdgcn_exp2f(st[g][sub][8 * s2 + 2 * j + 1]));
               const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[j]);
-              if (j & 1) l1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l1, false);
-              else l0 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l0, false);
+              if (j & 1) l1 = dot2acc(pr, one, l1);
+              else l0 = dot2acc(pr, one, l0);
             }
             pf[g][sub][s2] = *reinterpret_cast<bf16x8_t*>(w);
           }
@@ -267,9 +281,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
           const int sk = fa_swk(key);
 #pragma unroll
           for (int s = 0; s < 4; ++s)
-            st[g][sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            st[g][sub] = mfma32x32x16(
                 *reinterpret_cast<const bf16x8_t*>(kr + (((2 * s + hh) ^ sk) << 4)), qf[g][s],
-                s == 0 ? negm[g] : st[g][sub], 0, 0, 0);
+                s == 0 ? negm[g] : st[g][sub]);
         }
         if (kv0 + 64 > p.Skv) {
 #pragma unroll
@@ -361,7 +375,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
           const bf16x8_t af = *reinterpret_cast<bf16x8_t*>(&v8);
 #pragma unroll
           for (int g = 0; g < QG; ++g)
-            o[g][dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf[g][sub][s2], o[g][dh], 0, 0, 0);
+            o[g][dh] = mfma32x32x16(af, pf[g][sub][s2], o[g][dh]);
         }
       }
     FA_PRIO_OFF();
@@ -401,14 +415,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4 / QG,
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const uint2 bw = *reinterpret_cast<const uint2*>(vbr + 32 * half + d0);
-          a[4 * half + 0] += __uint_as_float(bw.x << 16); a[4 * half + 1] += __uint_as_float(bw.x & 0xffff0000u);
-          a[4 * half + 2] += __uint_as_float(bw.y << 16); a[4 * half + 3] += __uint_as_float(bw.y & 0xffff0000u);
+          a[4 * half + 0] += lo16f(bw.x); a[4 * half + 1] += hi16f(bw.x);
+          a[4 * half + 2] += lo16f(bw.y); a[4 * half + 3] += hi16f(bw.y);
           if (vbb) {
             const uint2 cw = *reinterpret_cast<const uint2*>(vbb + 32 * half + d0);
-            a[4 * half + 0] = fmaf(wb, __uint_as_float(cw.x << 16), a[4 * half + 0]);
-            a[4 * half + 1] = fmaf(wb, __uint_as_float(cw.x & 0xffff0000u), a[4 * half + 1]);
-            a[4 * half + 2] = fmaf(wb, __uint_as_float(cw.y << 16), a[4 * half + 2]);
-            a[4 * half + 3] = fmaf(wb, __uint_as_float(cw.y & 0xffff0000u), a[4 * half + 3]);
+            a[4 * half + 0] = fmaf(wb, lo16f(cw.x), a[4 * half + 0]);
+            a[4 * half + 1] = fmaf(wb, hi16f(cw.x), a[4 * half + 1]);
+            a[4 * half + 2] = fmaf(wb, lo16f(cw.y), a[4 * half + 2]);
+            a[4 * half + 3] = fmaf(wb, hi16f(cw.y), a[4 * half + 3]);
           }
         }
       }
@@ -478,7 +492,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
       uint32_t w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        w[j] = pack2(__uint_as_float(tw[j] << 16) * c, __uint_as_float(tw[j] & 0xffff0000u) * c);
+        w[j] = pack2(lo16f(tw[j]) * c, hi16f(tw[j]) * c);
       qf[qb][ks] = *reinterpret_cast<bf16x8_t*>(w);
     }
 
@@ -545,8 +559,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
           const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kt + koff[ks] + 2048 * kb);
 #pragma unroll
           for (int qb = 0; qb < 2; ++qb)
-            st[qb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qb][ks], ks == 0 ? negm[qb] : st[qb][kb],
-                                                                0, 0, 0);
+            st[qb][kb] = mfma16x16x32(kf, qf[qb][ks], ks == 0 ? negm[qb] : st[qb][kb]);
         }
       if (kv0 + 64 > p.Skv) {
 #pragma unroll
@@ -563,7 +576,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       auto expack = [&]() {
-        const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+        const bf16x2_t one = one2_16();
         float l0 = 0.0f, l1 = 0.0f;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -573,8 +586,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
             const f32x4_t& sv = st[qb][2 * t + (j >> 1)];
             w[j] = pack2(__builtin_amdgcn_exp2f(sv[2 * (j & 1)]), __builtin_amdgcn_exp2f(sv[2 * (j & 1) + 1]));
             const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, w[j]);
-            if (j & 1) l1 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l1, false);
-            else l0 = __builtin_amdgcn_fdot2_f32_bf16(pr, one, l0, false);
+            if (j & 1) l1 = dot2acc(pr, one, l1);
+            else l0 = dot2acc(pr, one, l0);
           }
           pf[t][qb] = *reinterpret_cast<bf16x8_t*>(w);
         }
@@ -622,7 +635,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
         const bf16x8_t af = __builtin_bit_cast(bf16x8_t, v8);
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
-          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, pf[t][qb], o[db][qb], 0, 0, 0);
+          o[db][qb] = mfma16x16x32(af, pf[t][qb], o[db][qb]);
       }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -657,14 +670,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
       for (int r = 0; r < 4; ++r) a[r] = o[db][qb][r] * inv;
       if (IP) {
         const uint2 bw = *reinterpret_cast<const uint2*>(vbr + d0);
-        a[0] += __uint_as_float(bw.x << 16); a[1] += __uint_as_float(bw.x & 0xffff0000u);
-        a[2] += __uint_as_float(bw.y << 16); a[3] += __uint_as_float(bw.y & 0xffff0000u);
+        a[0] += lo16f(bw.x); a[1] += hi16f(bw.x);
+        a[2] += lo16f(bw.y); a[3] += hi16f(bw.y);
         if (vbb) {
           const uint2 cw = *reinterpret_cast<const uint2*>(vbb + d0);
-          a[0] = fmaf(wb, __uint_as_float(cw.x << 16), a[0]);
-          a[1] = fmaf(wb, __uint_as_float(cw.x & 0xffff0000u), a[1]);
-          a[2] = fmaf(wb, __uint_as_float(cw.y << 16), a[2]);
-          a[3] = fmaf(wb, __uint_as_float(cw.y & 0xffff0000u), a[3]);
+          a[0] = fmaf(wb, lo16f(cw.x), a[0]);
+          a[1] = fmaf(wb, hi16f(cw.x), a[1]);
+          a[2] = fmaf(wb, lo16f(cw.y), a[2]);
+          a[3] = fmaf(wb, hi16f(cw.y), a[3]);
         }
       }
       *reinterpret_cast<uint2*>(ob + d0) = make_uint2(pack2(a[0], a[1]), pack2(a[2], a[3]));
@@ -776,8 +789,8 @@ __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTempo
     f32x4_t st = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8_t*>(&kv[ks]),
-                                                   *reinterpret_cast<const bf16x8_t*>(&qv[ks]), st, 0, 0, 0);
+      st = mfma16x16x32(*reinterpret_cast<const bf16x8_t*>(&kv[ks]),
+                                                   *reinterpret_cast<const bf16x8_t*>(&qv[ks]), st);
     // softmax over the keys of query fr: keys 4 g + i here, the other 12 in lanes fr + 16 k
     float sc[4], mx = -INFINITY;
 #pragma unroll
@@ -802,7 +815,7 @@ __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTempo
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
       const short4_t a = *reinterpret_cast<const short4_t*>(&vt[(16 * dt + fr) * TM_VLD + 4 * g]);
-      const f32x4_t o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, f32x4_t{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+      const f32x4_t o = mfma16x16x16_s4(a, pb, f32x4_t{0.0f, 0.0f, 0.0f, 0.0f});
       // o[i] = O[query fr][d = 16 dt + 4 g + i]
       if (fok)
         *reinterpret_cast<uint2*>(orow + 16 * dt) =

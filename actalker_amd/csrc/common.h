@@ -5,21 +5,79 @@
 #include <stdint.h>
 #include "../../include/actalker_hip.h"
 
-typedef uint16_t bf16_t;                                          // raw bf16 bits in HBM
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));      // MFMA A/B fragment
+// Activation precision. The kernels are written once over a 16-bit activation type and built twice
+// (Makefile): libactalker_hip.so with bf16 activations (ACTH_F16 = 0, the default path) and
+// libactalker_hip_f16.so with fp16 activations (ACTH_F16 = 1: the reference's shipped weight_dtype,
+// config/inference.yaml:66). Weights, activations and 16-bit MFMA operands share that type; accumulation,
+// statistics and the sampler state stay fp32 in both builds. The names below keep "bf16" for the 16-bit
+// activation type in either build (`bf16_t` is its raw bits in HBM).
+#ifndef ACTH_F16
+#define ACTH_F16 0
+#endif
+typedef uint16_t bf16_t;                                          // raw 16-bit activation bits in HBM
+#if ACTH_F16
+typedef _Float16 act16_t;
+#else
+typedef __bf16 act16_t;
+#endif
+typedef act16_t bf16x8_t __attribute__((ext_vector_type(8)));     // MFMA A/B fragment
 typedef float f32x16_t __attribute__((ext_vector_type(16)));      // 32x32 MFMA accumulator
 typedef float f32x4_t __attribute__((ext_vector_type(4)));        // 16x16 MFMA accumulator
+
+// the 16-bit MFMAs over the activation type (fp16 runs at the bf16 rate on gfx950)
+__device__ __forceinline__ f32x4_t mfma16x16x32(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+#if ACTH_F16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+__device__ __forceinline__ f32x16_t mfma32x32x16(bf16x8_t a, bf16x8_t b, f32x16_t c) {
+#if ACTH_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+// the two 16-bit values packed in a 32-bit word as floats (low half, high half)
+__device__ __forceinline__ float lo16f(uint32_t w) {
+#if ACTH_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+#else
+  return __uint_as_float(w << 16);
+#endif
+}
+
+__device__ __forceinline__ float hi16f(uint32_t w) {
+#if ACTH_F16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+#else
+  return __uint_as_float(w & 0xffff0000u);
+#endif
+}
 
 #define ACTH_CHECK_LAUNCH()                                  \
   do {                                                       \
     if (hipGetLastError() != hipSuccess) return ACTH_ELAUNCH; \
   } while (0)
 
-__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ float bf2f(bf16_t v) {
+#if ACTH_F16
+  return (float)__builtin_bit_cast(_Float16, v);
+#else
+  return __uint_as_float(((uint32_t)v) << 16);
+#endif
+}
 
 __device__ __forceinline__ bf16_t f2bf(float f) {
+#if ACTH_F16
+  return __builtin_bit_cast(uint16_t, (_Float16)f);             // RNE
+#else
   // lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
   return __bfloat16_as_ushort(__float2bfloat16(f));
+#endif
 }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
@@ -90,21 +148,32 @@ __device__ __forceinline__ float softplus_f(float x) {
   return x > 20.0f ? x : log1pf(__expf(x));
 }
 
-// unpack 8 bf16 held in a uint4 into floats
+// unpack 8 16-bit activations held in a uint4 into floats
 __device__ __forceinline__ void unpack8(const uint4 v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+  f[0] = lo16f(v.x); f[1] = hi16f(v.x);
+  f[2] = lo16f(v.y); f[3] = hi16f(v.y);
+  f[4] = lo16f(v.z); f[5] = hi16f(v.z);
+  f[6] = lo16f(v.w); f[7] = hi16f(v.w);
 }
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef act16_t bf16x2_t __attribute__((ext_vector_type(2)));
 
-// two floats -> packed bf16 pair (low = a) in ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving); two
-// scalar f2bf conversions + shift + or cost three extra VALU per pair in every epilogue
+// two floats -> packed 16-bit pair (low = a) in ONE v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32 (RNE); two scalar
+// f2bf conversions + shift + or cost three extra VALU per pair in every epilogue
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
+
+// packed pair of ones, and dot2 accumulation over packed 16-bit pairs (v_dot2_f32_bf16 / v_dot2c_f32_f16)
+__device__ __forceinline__ bf16x2_t one2_16() { return (bf16x2_t){(act16_t)1.0f, (act16_t)1.0f}; }
+
+__device__ __forceinline__ float dot2acc(bf16x2_t a, bf16x2_t b, float c) {
+#if ACTH_F16
+  return __builtin_amdgcn_fdot2(a, b, c, false);
+#else
+  return __builtin_amdgcn_fdot2_f32_bf16(a, b, c, false);
+#endif
 }
 
 __device__ __forceinline__ uint4 pack8(const float* f) {

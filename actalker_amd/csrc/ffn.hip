@@ -199,7 +199,7 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
       // statistics over the lane pair's row (hi = 0 / 1 hold the two channel halves) by bf16 dot2 into fp32:
       // sum and sum of squares straight from the packed row, no unpacked copy of it live (E[x^2] - mean^2,
       // as the attention kernels' LayerNorms)
-      const bf16x2_t one2 = __builtin_bit_cast(bf16x2_t, 0x3f803f80u);
+      const bf16x2_t one2 = one2_16();
       float sm = 0.0f, q = 0.0f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bf16x2_t v2 = __builtin_bit_cast(bf16x2_t, w[j]);
-          sm = __builtin_amdgcn_fdot2_f32_bf16(v2, one2, sm, false);
-          q = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, q, false);
+          sm = dot2acc(v2, one2, sm);
+          q = dot2acc(v2, v2, q);
         }
       }
       sm += __shfl_xor(sm, 32, 64);
@@ -306,11 +306,11 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
       if constexpr (s == KS) __builtin_amdgcn_s_setprio(0);
       if constexpr (DN && s == KS - 6) hpar = *reinterpret_cast<const bf16x8_t*>(hxr);
       if constexpr (s < KS) {
-        if constexpr (UP) u = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s & 3], xf[s], u, 0, 0, 0);
+        if constexpr (UP) u = mfma32x32x16(fr[s & 3], xf[s], u);
       } else {
         if constexpr (DN) {
           constexpr int f = (s - KS) >> 1, own = ((s - KS) & 1) == 0;
-          acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s & 3], own ? hown : hpar, acc[f], 0, 0, 0);
+          acc[f] = mfma32x32x16(fr[s & 3], own ? hown : hpar, acc[f]);
         }
         if constexpr (UP && DN && s >= KS + 1 && s < KS + 9) gate(s - KS - 1);
       }

@@ -121,10 +121,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(const ActhGemmDesc p,
       const bf16x8_t a1 = *reinterpret_cast<const bf16x8_t*>(sA + ar1 * 128 + ((c ^ (ar1 & 7)) << 4));
       const bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(sB + br0 * 128 + ((c ^ (br0 & 7)) << 4));
       const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(sB + br1 * 128 + ((c ^ (br1 & 7)) << 4));
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[1][1], 0, 0, 0);
+      acc[0][0] = mfma32x32x16(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32x32x16(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32x32x16(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32x32x16(a1, b1, acc[1][1]);
     }
     // next tile landed (this wave's DMAs) and every wave is done reading `cur`
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

@@ -205,7 +205,7 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(const ActhGemmDesc p, u
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
       }
       // next K tile landed (this wave's DMAs) and every wave is done reading `cur`
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

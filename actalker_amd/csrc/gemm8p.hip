@@ -323,8 +323,8 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       for (int i = 0; i < TMQ; ++i)
 #pragma unroll
         for (int j = 0; j < TNQ; ++j)
-          c[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], c[i][j], 0, 0, 0)
-                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
+          c[i][j] = TR ? mfma16x16x32(bfr[j][s], af[i][s], c[i][j])
+                       : mfma16x16x32(af[i][s], bfr[j][s], c[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -697,13 +697,13 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
             }
             if (RES) {
               const uint2 t = rq[i * TNQ + j];
-              v[0] += __uint_as_float(t.x << 16); v[1] += __uint_as_float(t.x & 0xffff0000u);
-              v[2] += __uint_as_float(t.y << 16); v[3] += __uint_as_float(t.y & 0xffff0000u);
+              v[0] += lo16f(t.x); v[1] += hi16f(t.x);
+              v[2] += lo16f(t.y); v[3] += hi16f(t.y);
             }
             if (MIXB) {
               const uint2 t = mq[i * TNQ + j];
-              const float m4[4] = {__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xffff0000u),
-                                   __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xffff0000u)};
+              const float m4[4] = {lo16f(t.x), hi16f(t.x),
+                                   lo16f(t.y), hi16f(t.y)};
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = p.mix_alpha * m4[e] + (1.0f - p.mix_alpha) * v[e];
             }

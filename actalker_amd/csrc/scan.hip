@@ -126,8 +126,8 @@ __global__ __launch_bounds__(SC_THREADS) void scan_kernel(const ActhScanDesc p) 
             v = *reinterpret_cast<const float4*>((const float*)p.delta + o);
           } else {
             const uint2 r2 = *reinterpret_cast<const uint2*>((const bf16_t*)p.delta + o);
-            v = make_float4(__uint_as_float(r2.x << 16), __uint_as_float(r2.x & 0xffff0000u),
-                            __uint_as_float(r2.y << 16), __uint_as_float(r2.y & 0xffff0000u));
+            v = make_float4(lo16f(r2.x), hi16f(r2.x),
+                            lo16f(r2.y), hi16f(r2.y));
           }
         }
         pd[e] = v;
@@ -395,8 +395,8 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
             v = *reinterpret_cast<const float4*>((const float*)p.delta + o);
           } else {
             const uint2 r2 = *reinterpret_cast<const uint2*>((const bf16_t*)p.delta + o);
-            v = make_float4(__uint_as_float(r2.x << 16), __uint_as_float(r2.x & 0xffff0000u),
-                            __uint_as_float(r2.y << 16), __uint_as_float(r2.y & 0xffff0000u));
+            v = make_float4(lo16f(r2.x), hi16f(r2.x),
+                            lo16f(r2.y), hi16f(r2.y));
           }
         }
         pd[e] = v;
@@ -411,8 +411,8 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
         const int idx = t + e * NT, tt = idx / XQ, c4 = (idx - tt * XQ) * 4;
         if (tt < SC_T) {
           const uint2 q = pxh[S][e];
-          float4 v = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
-                                 __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+          float4 v = make_float4(lo16f(q.x), hi16f(q.x),
+                                 lo16f(q.y), hi16f(q.y));
           if (R4 > R && c4 + 4 == R4) {          // dt padding columns are ignored: zero (they meet zero weights)
             if (R4 - R >= 1) v.w = 0.f;
             if (R4 - R >= 2) v.z = 0.f;
@@ -723,8 +723,8 @@ __global__ __launch_bounds__(SQ_NT, R <= 40 ? SQ_OCC : SQ_OCC - 1) void scan_qua
       const int idx = t + e * SQ_NT, xt = idx / XQ, xc = (idx - xt * XQ) * 4;
       if (xt < 16)
         *reinterpret_cast<float4*>(&xs[xt * WP + xc]) =
-            make_float4(__uint_as_float(px[S][e].x << 16), __uint_as_float(px[S][e].x & 0xffff0000u),
-                        __uint_as_float(px[S][e].y << 16), __uint_as_float(px[S][e].y & 0xffff0000u));
+            make_float4(lo16f(px[S][e].x), hi16f(px[S][e].x),
+                        lo16f(px[S][e].y), hi16f(px[S][e].y));
     }
     *reinterpret_cast<uint2*>(&us[ut * SQ_UP + uc]) = pu[S];
   };

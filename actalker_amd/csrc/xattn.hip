@@ -89,10 +89,10 @@ __global__ __launch_bounds__(1024) void ip_fold_kernel(const ActhIpFoldDesc p) {
   for (int d = 0; d < 64; ++d) {
     const uint2 q2 = *reinterpret_cast<const uint2*>(wq + (size_t)d * p.ldwq);
     const uint2 o2 = *reinterpret_cast<const uint2*>(wo + (size_t)d * p.ldwo);
-    const float q4[4] = {__uint_as_float(q2.x << 16), __uint_as_float(q2.x & 0xffff0000u),
-                         __uint_as_float(q2.y << 16), __uint_as_float(q2.y & 0xffff0000u)};
-    const float o4[4] = {__uint_as_float(o2.x << 16), __uint_as_float(o2.x & 0xffff0000u),
-                         __uint_as_float(o2.y << 16), __uint_as_float(o2.y & 0xffff0000u)};
+    const float q4[4] = {lo16f(q2.x), hi16f(q2.x),
+                         lo16f(q2.y), hi16f(q2.y)};
+    const float o4[4] = {lo16f(o2.x), hi16f(o2.x),
+                         lo16f(o2.y), hi16f(o2.y)};
     const float4 k0 = *reinterpret_cast<const float4*>(&kt[d][8 * jg]);
     const float4 k1 = *reinterpret_cast<const float4*>(&kt[d][8 * jg + 4]);
     const float4 v0 = *reinterpret_cast<const float4*>(&vt[d][8 * jg]);
@@ -127,8 +127,8 @@ __global__ __launch_bounds__(1024) void ip_fold_kernel(const ActhIpFoldDesc p) {
       bpart = fmaf(b4[c], kk, bpart);
     }
     const uint2 kb = make_uint2(pack2(k[0], k[1]), pack2(k[2], k[3]));
-    gpart = __uint_as_float(kb.x << 16) + __uint_as_float(kb.x & 0xffff0000u) + __uint_as_float(kb.y << 16) +
-            __uint_as_float(kb.y & 0xffff0000u);
+    gpart = lo16f(kb.x) + hi16f(kb.x) + lo16f(kb.y) +
+            hi16f(kb.y);
     *reinterpret_cast<uint2*>(kp + (size_t)j * C) = kb;
     *reinterpret_cast<uint2*>(vp + (size_t)j * C) = make_uint2(pack2(av[j][0], av[j][1]), pack2(av[j][2], av[j][3]));
     red[(jg * 8 + j) * ncg + cg] = make_float2(gpart, bpart);
@@ -304,14 +304,14 @@ __global__ __launch_bounds__(256, 2) void xattn_kernel(const ActhXattnDesc p, un
     wait_chunk(I0{});
     stamp(1);
     {
-      const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+      const bf16x2_t one = one2_16();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bf16x2_t pair = {xf[ks][2 * e], xf[ks][2 * e + 1]};
-          s1 = __builtin_amdgcn_fdot2_f32_bf16(pair, one, s1, false);
-          s2 = __builtin_amdgcn_fdot2_f32_bf16(pair, pair, s2, false);
+          s1 = dot2acc(pair, one, s1);
+          s2 = dot2acc(pair, pair, s2);
         }
     }
     {
@@ -359,8 +359,8 @@ __global__ __launch_bounds__(256, 2) void xattn_kernel(const ActhXattnDesc p, un
       for (int ks = 0; ks < KS; ++ks) {
         const bf16x8_t cur = fr[ks & 3];
         if (ks + 4 < KS) fr[ks & 3] = *reinterpret_cast<const bf16x8_t*>(kb + a1[ks & 3] + ((ks + 4) >> 2) * 128);
-        if (ks & 1) u1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, xf[ks], u1, 0, 0, 0);
-        else u = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, xf[ks], u, 0, 0, 0);
+        if (ks & 1) u1 = mfma32x32x16(cur, xf[ks], u1);
+        else u = mfma32x32x16(cur, xf[ks], u);
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) u[e] += u1[e];
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256, 2) void xattn_kernel(const ActhXattnDesc p, un
       for (int st = 0; st < 2 * HF; ++st) {
         const int s2i = st / HF, f = st % HF;
         if (st + 1 < 2 * HF) vnxt = vread((st + 1) / HF, (st + 1) % HF);
-        acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vcur), pb[s2i], acc[f], 0, 0, 0);
+        acc[f] = mfma32x32x16(__builtin_bit_cast(bf16x8_t, vcur), pb[s2i], acc[f]);
         vcur = vnxt;
       }
     });
@@ -462,17 +462,17 @@ __global__ __launch_bounds__(256, 2) void xattn_kernel(const ActhXattnDesc p, un
         const uint2 hv = *reinterpret_cast<const uint2*>(trow + c0);
         const float4 bs = *reinterpret_cast<const float4*>(&sbase[c0]);
         const float4 vw = *reinterpret_cast<const float4*>(&svbw[c0]);
-        const float x0 = __uint_as_float(hv.x << 16), x1 = __uint_as_float(hv.x & 0xffff0000u);
-        const float x2 = __uint_as_float(hv.y << 16), x3 = __uint_as_float(hv.y & 0xffff0000u);
+        const float x0 = lo16f(hv.x), x1 = hi16f(hv.x);
+        const float x2 = lo16f(hv.y), x3 = hi16f(hv.y);
         const uint2 o = make_uint2(pack2(x0 + fmaf(wb, vw.x, fmaf(wa, acc[f][4 * jb + 0], bs.x)),
                                          x1 + fmaf(wb, vw.y, fmaf(wa, acc[f][4 * jb + 1], bs.y))),
                                    pack2(x2 + fmaf(wb, vw.z, fmaf(wa, acc[f][4 * jb + 2], bs.z)),
                                          x3 + fmaf(wb, vw.w, fmaf(wa, acc[f][4 * jb + 3], bs.w))));
         *reinterpret_cast<uint2*>(trow + c0) = o;
-        acc[f][4 * jb + 0] = __uint_as_float(o.x << 16);
-        acc[f][4 * jb + 1] = __uint_as_float(o.x & 0xffff0000u);
-        acc[f][4 * jb + 2] = __uint_as_float(o.y << 16);
-        acc[f][4 * jb + 3] = __uint_as_float(o.y & 0xffff0000u);
+        acc[f][4 * jb + 0] = lo16f(o.x);
+        acc[f][4 * jb + 1] = hi16f(o.x);
+        acc[f][4 * jb + 2] = lo16f(o.y);
+        acc[f][4 * jb + 3] = hi16f(o.y);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           s1 += acc[f][4 * jb + r];

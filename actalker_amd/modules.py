@@ -40,6 +40,8 @@ class Packed(nn.Module):
     """Mixin: per-module cache of kernel-layout weights."""
 
     def _pk(self, key, fn):
+        # kernel layouts are per activation dtype (bf16 / fp16 builds, ops.compute_dtype)
+        key = (key, ops.act_dtype())
         cache = self.__dict__.setdefault("_acth_cache", {})
         v = cache.get(key)
         if v is None:
@@ -53,7 +55,8 @@ class Packed(nn.Module):
 
 
 def _bf(w: torch.Tensor) -> torch.Tensor:
-    return w.detach().to(torch.bfloat16).contiguous()
+    """A weight in the current activation dtype (bf16, or fp16 inside ops.compute_dtype(torch.float16))."""
+    return w.detach().to(ops.act_dtype()).contiguous()
 
 
 def _f32(b: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -374,6 +377,7 @@ def _versioned_pack(mod: nn.Module, key, tensors, fn):
     themselves: a replaced Parameter (a fresh tensor that the caching allocator may place at the freed
     address, with _version 0 again) never matches a stale entry."""
     cache = mod.__dict__.setdefault("_acth_vcache", {})
+    key = (key, ops.act_dtype())         # one layout per activation dtype (ops.compute_dtype)
     ver = tuple((t.data_ptr(), t._version) for t in tensors)
     hit = cache.get(key)
     if hit is None or hit[0] != ver or any(r() is not t for r, t in zip(hit[2], tensors)):
@@ -663,7 +667,8 @@ class SS2D_Unit(nn.Module):
 
     def packed(self):
         c = self.__dict__.setdefault("_acth_cache", {})
-        if "p" not in c:
+        key = ("p", ops.act_dtype())
+        if key not in c:
             with torch.no_grad():
                 K, R, Din = self.num_direction, self.dt_rank, self.d_inner
                 R4 = (R + 3) // 4 * 4
@@ -671,14 +676,14 @@ class SS2D_Unit(nn.Module):
                 if R4 != R:      # [dt (R) | 0 (R4 - R) | B | C] per direction: 8-byte aligned bf16 rows
                     pad = torch.zeros((K, R4 - R, Din), device=xw.device, dtype=xw.dtype)
                     xw = torch.cat([xw[:, :R], pad, xw[:, R:]], dim=1)
-                c["p"] = dict(
+                c[key] = dict(
                     xproj=_bf(self.x_proj_weight.reshape(-1, self.d_inner)),
                     xproj_pad=_bf(xw.reshape(-1, Din)),
                     dt_w=_f32(self.dt_projs_weight),
                     dt_b=_f32(self.dt_projs_bias),
                     A_log=_f32(self.A_logs),
                     D=_f32(self.Ds))
-        return c["p"]
+        return c[key]
 
     def _acth_invalidate(self):
         self.__dict__["_acth_cache"] = {}
@@ -743,7 +748,7 @@ class SS2D_cond_v10(nn.Module):
             # nothing selected: the scan runs on [ID, cond] only and its output is discarded
             return dict(mode=0, x=ops.gemm(h, in_proj.w()))
         L = n_sel + 1 + n_cond
-        u = torch.empty((BF * L, Din), device=h.device, dtype=torch.bfloat16)
+        u = torch.empty((BF * L, Din), device=h.device, dtype=ops.act_dtype())
         br = {}
         if identity:
             ops.gemm(h, in_proj.w(), out=u, orow=(S, L, 0))

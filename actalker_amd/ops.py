@@ -1,14 +1,18 @@
-"""Torch-tensor front end of the C ABI (libactalker_hip.so).
+"""Torch-tensor front end of the C ABI (libactalker_hip.so / libactalker_hip_f16.so).
 
 Every function here validates shapes on the host, allocates its output with torch's caching
 allocator (device memory is torch's; compute is ours) and launches on
-``torch.cuda.current_stream()``. Activations are token-major 2-D tensors ``(rows, C)`` in bf16.
+``torch.cuda.current_stream()``. Activations are token-major 2-D tensors ``(rows, C)`` in the current
+activation dtype: bf16 by default, fp16 inside ``compute_dtype(torch.float16)`` -- the same kernels built
+with fp16 activations (the reference's shipped ``weight_dtype: 'fp16'``, config/inference.yaml:66).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import math
+import threading
 from typing import Optional, Sequence
 
 import torch
@@ -16,6 +20,29 @@ import torch
 from . import _lib
 
 ACT_NONE, ACT_SILU, ACT_GEGLU, ACT_GELU, ACT_RELU = 0, 1, 2, 3, 4
+
+_TLS = threading.local()        # per-thread stack: concurrent UNet calls (LoopConfig.concurrent_calls) nest safely
+
+
+def act_dtype() -> torch.dtype:
+    """The activation dtype the ops compute in (and the library they launch from)."""
+    st = getattr(_TLS, "stack", None)
+    return st[-1] if st else torch.bfloat16
+
+
+@contextlib.contextmanager
+def compute_dtype(dtype: torch.dtype):
+    """Run the ops inside the block with ``dtype`` activations (torch.bfloat16 or torch.float16)."""
+    if dtype not in (torch.bfloat16, torch.float16):
+        raise _lib.ActhError(f"compute dtype must be bfloat16 or float16, got {dtype}")
+    st = getattr(_TLS, "stack", None)
+    if st is None:
+        st = _TLS.stack = []
+    st.append(dtype)
+    try:
+        yield
+    finally:
+        st.pop()
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -60,16 +87,16 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
     A modes: dense (a is (M, K1) [+ a2 (M, K-K1)]), ``conv=dict(H, W, Ho, Wo, stride, upsample, B)``
     (a is the NHWC image as (B*H*W, C1) [+ a2]), ``temporal=dict(F, S)`` (a is (M, C1) rows).
     """
-    lib = _lib.load()
-    _need(w, torch.bfloat16, "gemm weight")
+    lib = _lib.load(act_dtype())
+    _need(w, act_dtype(), "gemm weight")
     N, K = w.shape
     d = _lib.GemmDesc()
     d.A = a.data_ptr()
     d.lda = _rows(a, "gemm A")
-    _need(a, torch.bfloat16, "gemm A")
+    _need(a, act_dtype(), "gemm A")
     c1 = a.shape[1] if k1 is None else k1
     if a2 is not None:
-        _need(a2, torch.bfloat16, "gemm A2")
+        _need(a2, act_dtype(), "gemm A2")
         d.A2 = a2.data_ptr()
         d.lda2 = _rows(a2, "gemm A2")
     d.K1 = c1 if a2 is not None else (1 << 30)
@@ -119,7 +146,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
         d.rb_div = rb_div
         d.ldrb = _rows(rowbias, "gemm rowbias")
     if residual is not None:
-        _need(residual, torch.bfloat16, "gemm residual")
+        _need(residual, act_dtype(), "gemm residual")
         if residual.dim() != 2 or residual.shape[1] < n_out:
             raise _lib.ActhError(f"gemm: residual {tuple(residual.shape)} narrower than N={n_out}")
         d.R = residual.data_ptr()
@@ -138,7 +165,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
         elif residual.shape[0] < M:
             raise _lib.ActhError(f"gemm: residual has {residual.shape[0]} rows < M={M}")
     if mix is not None:
-        _need(mix, torch.bfloat16, "gemm mix")
+        _need(mix, act_dtype(), "gemm mix")
         if mix.dim() != 2 or mix.shape[0] < M or mix.shape[1] < n_out:
             raise _lib.ActhError(f"gemm: mix {tuple(mix.shape)} too small for ({M}, {n_out})")
         d.MIX = mix.data_ptr()
@@ -149,9 +176,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
     if out is None:
         if orow is not None:
             raise _lib.ActhError("gemm: orow remap needs an explicit output tensor")
-        out = torch.empty((M, n_out), device=a.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        out = torch.empty((M, n_out), device=a.device, dtype=torch.float32 if out_f32 else act_dtype())
     else:
-        _need(out, torch.float32 if out_f32 else torch.bfloat16, "gemm out")
+        _need(out, torch.float32 if out_f32 else act_dtype(), "gemm out")
     d.out_f32 = int(out_f32)
     d.C = out.data_ptr()
     d.ldc = _rows(out, "gemm out")
@@ -184,12 +211,12 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, B: int, H: int, W: int, *, x2=None
 # ------------------------------------------------------------------------------------------
 def flash_attn(qkv: torch.Tensor, nbatch: int, S: int, heads: int, out: Optional[torch.Tensor] = None):
     """Self-attention over S tokens per batch on fused [q|k|v] rows (nbatch*S, 3C)."""
-    lib = _lib.load()
-    _need(qkv, torch.bfloat16, "flash_attn qkv")
+    lib = _lib.load(act_dtype())
+    _need(qkv, act_dtype(), "flash_attn qkv")
     C = heads * 64
     ld = _rows(qkv, "flash_attn qkv")
     if out is None:
-        out = torch.empty((nbatch * S, C), device=qkv.device, dtype=torch.bfloat16)
+        out = torch.empty((nbatch * S, C), device=qkv.device, dtype=act_dtype())
     d = _lib.AttnDesc()
     base = qkv.data_ptr()
     d.q, d.k, d.v, d.o = base, base + 2 * C, base + 4 * C, out.data_ptr()
@@ -204,10 +231,10 @@ def flash_attn(qkv: torch.Tensor, nbatch: int, S: int, heads: int, out: Optional
 
 
 def temporal_attn(qkv: torch.Tensor, B: int, F: int, S: int, heads: int, out=None):
-    lib = _lib.load()
-    _need(qkv, torch.bfloat16, "temporal_attn qkv")
+    lib = _lib.load(act_dtype())
+    _need(qkv, act_dtype(), "temporal_attn qkv")
     if out is None:
-        out = torch.empty((B * F * S, heads * 64), device=qkv.device, dtype=torch.bfloat16)
+        out = torch.empty((B * F * S, heads * 64), device=qkv.device, dtype=act_dtype())
     d = _lib.TemporalAttnDesc()
     d.qkv, d.ldqkv = qkv.data_ptr(), _rows(qkv, "temporal_attn qkv")
     d.o, d.ldo = out.data_ptr(), _rows(out, "temporal_attn out")
@@ -219,9 +246,9 @@ def temporal_attn(qkv: torch.Tensor, B: int, F: int, S: int, heads: int, out=Non
 
 def ip_attn(vbase: torch.Tensor, M: int, heads: int, rows_per_ctx: int, S: int, *, q=None, kv=None, nkeys=32,
             vb=None, mask_a=None, mask_b=None, sa=1.0, sb=1.0, out=None):
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     if out is None:
-        out = torch.empty((M, heads * 64), device=vbase.device, dtype=torch.bfloat16)
+        out = torch.empty((M, heads * 64), device=vbase.device, dtype=act_dtype())
     d = _lib.IpAttnDesc()
     if kv is not None:
         d.q, d.ldq = q.data_ptr(), _rows(q, "ip_attn q")
@@ -255,11 +282,11 @@ def ip_fold(wq: torch.Tensor, woT: torch.Tensor, bo: Optional[torch.Tensor], vid
     in front, folded in): returns (kp, vp, gb, base, vbw) -- K'' / V' (nctx*H*32, C) bf16 and the per-key LN2
     constants gb (nctx*H*32, 2) fp32 (None without ``kv``), base = bo + Wo v_id and vbw = Wo v_vasa (nctx, C)
     fp32 (vbw None without ``vb``)."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     C = wq.shape[0]
     nctx = vid.shape[0]
     for t, nm in ((wq, "wq"), (woT, "woT"), (vid, "vid")):
-        _need(t, torch.bfloat16, f"ip_fold {nm}")
+        _need(t, act_dtype(), f"ip_fold {nm}")
     if tuple(wq.shape) != (C, C) or tuple(woT.shape) != (C, C) or vid.shape[1] != C or heads * 64 != C:
         raise _lib.ActhError(f"ip_fold: wq {tuple(wq.shape)} woT {tuple(woT.shape)} vid {tuple(vid.shape)} H={heads}")
     d = _lib.IpFoldDesc()
@@ -275,18 +302,18 @@ def ip_fold(wq: torch.Tensor, woT: torch.Tensor, bo: Optional[torch.Tensor], vid
     if norm2 is not None:
         d.g2, d.b2 = _p(norm2[0]), _p(norm2[1])
     if vb is not None:
-        _need(vb, torch.bfloat16, "ip_fold vb")
+        _need(vb, act_dtype(), "ip_fold vb")
         if tuple(vb.shape) != (nctx, C):
             raise _lib.ActhError(f"ip_fold: vb {tuple(vb.shape)} for {nctx} contexts")
         d.vb, d.ldvb = vb.data_ptr(), _rows(vb, "ip_fold vb")
         vbw = torch.empty((nctx, C), device=vid.device, dtype=torch.float32)
         d.vbw = vbw.data_ptr()
     if kv is not None:
-        _need(kv, torch.bfloat16, "ip_fold kv")
+        _need(kv, act_dtype(), "ip_fold kv")
         if kv.shape[0] != nctx * 32 or kv.shape[1] < 2 * C:
             raise _lib.ActhError(f"ip_fold: kv {tuple(kv.shape)} for {nctx} contexts x 32 keys, C={C}")
         d.kv, d.ldkv = kv.data_ptr(), _rows(kv, "ip_fold kv")
-        kp = torch.empty((nctx * heads * 32, C), device=vid.device, dtype=torch.bfloat16)
+        kp = torch.empty((nctx * heads * 32, C), device=vid.device, dtype=act_dtype())
         vp = torch.empty_like(kp)
         gb = torch.empty((nctx * heads * 32, 2), device=vid.device, dtype=torch.float32)
         d.kp, d.vp, d.gb = kp.data_ptr(), vp.data_ptr(), gb.data_ptr()
@@ -305,8 +332,8 @@ def xattn(h: torch.Tensor, eps2: float, norm3, base: torch.Tensor, *, heads: int
     ``eps2`` = norm2's eps (its weight / bias live in K'' / gb), ``norm3`` = (gamma fp32, beta fp32, eps), or
     None when the consumer (geglu_ffn's ``ln``) normalises itself -- then the second result is None;
     K'' / V' / gb / base / vbw from :func:`ip_fold`."""
-    lib = _lib.load()
-    _need(h, torch.bfloat16, "xattn h")
+    lib = _lib.load(act_dtype())
+    _need(h, act_dtype(), "xattn h")
     M, C = h.shape
     if C not in XATTN_C or M % rows_per_ctx or rows_per_ctx % XATTN_ROWS:
         raise _lib.ActhError(f"xattn: M={M} C={C} rows_per_ctx={rows_per_ctx}")
@@ -357,13 +384,13 @@ def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p
     ``w1``/``b1`` from modules.pack_geglu, ``w2p`` from modules.pack_ffn_w2. ``ln`` = (gamma, beta, eps):
     x' = LayerNorm(x) computed in the kernel (else x' = x). ``add`` (rows, C) bf16: x and the residual each
     get bf16(. + add[row // add_div]) first (not with ``mix``)."""
-    lib = _lib.load()
-    _need(x, torch.bfloat16, "geglu_ffn x")
+    lib = _lib.load(act_dtype())
+    _need(x, act_dtype(), "geglu_ffn x")
     M, C = x.shape
     if C not in FFN_FUSED_C:
         raise _lib.ActhError(f"geglu_ffn: C={C} not in {FFN_FUSED_C}")
-    _need(w1, torch.bfloat16, "geglu_ffn w1")
-    _need(w2p, torch.bfloat16, "geglu_ffn w2")
+    _need(w1, act_dtype(), "geglu_ffn w1")
+    _need(w2p, act_dtype(), "geglu_ffn w2")
     if tuple(w1.shape) != (8 * C, C) or tuple(w2p.shape) != (C, 4 * C):
         raise _lib.ActhError(f"geglu_ffn: weights {tuple(w1.shape)} / {tuple(w2p.shape)} for C={C}")
     for t, nm in ((b1, "b1"), (b2, "b2")):
@@ -373,11 +400,11 @@ def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p
                 raise _lib.ActhError(f"geglu_ffn {nm}: {tuple(t.shape)}")
     for t, nm in ((residual, "residual"), (mix, "mix")):
         if t is not None:
-            _need(t, torch.bfloat16, f"geglu_ffn {nm}")
+            _need(t, act_dtype(), f"geglu_ffn {nm}")
             if t.dim() != 2 or t.shape[0] < M or t.shape[1] < C:
                 raise _lib.ActhError(f"geglu_ffn {nm}: {tuple(t.shape)} for ({M}, {C})")
     if out is None:
-        out = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((M, C), device=x.device, dtype=act_dtype())
     elif out.shape[0] < M or out.shape[1] < C:
         raise _lib.ActhError(f"geglu_ffn out: {tuple(out.shape)} for ({M}, {C})")
     d = _lib.FfnDesc()
@@ -397,7 +424,7 @@ def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p
                 raise _lib.ActhError("geglu_ffn ln: gamma / beta must be contiguous fp32 of C entries")
         d.ln_g, d.ln_b, d.ln_eps, d.ln = _p(g), _p(b), float(eps), 1
     if add is not None:
-        _need(add, torch.bfloat16, "geglu_ffn add")
+        _need(add, act_dtype(), "geglu_ffn add")
         if mix is not None or add_div <= 0 or add_div % 64 or add.dim() != 2 or add.shape[1] < C or \
                 add.shape[0] * add_div < M:
             raise _lib.ActhError(f"geglu_ffn add: {tuple(add.shape)} add_div={add_div} for M={M}")
@@ -409,11 +436,11 @@ def geglu_ffn(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2p
 # ------------------------------------------------------------------------------------------
 def layernorm(x: torch.Tensor, gamma, beta, eps: float = 1e-5, *, add=None, add_div: int = 1,
               sum_out: Optional[torch.Tensor] = None, out=None):
-    lib = _lib.load()
-    _need(x, torch.bfloat16, "layernorm x")
+    lib = _lib.load(act_dtype())
+    _need(x, act_dtype(), "layernorm x")
     M, C = x.shape
     if out is None:
-        out = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((M, C), device=x.device, dtype=act_dtype())
     d = _lib.LayerNormDesc()
     d.x, d.ldx = x.data_ptr(), _rows(x, "layernorm x")
     if add is not None:
@@ -432,13 +459,13 @@ def layernorm(x: torch.Tensor, gamma, beta, eps: float = 1e-5, *, add=None, add_
 def groupnorm(x: torch.Tensor, gamma, beta, eps: float, rows_per_stat: int, *, x2=None, silu=False, groups=32,
               out=None, relu=False, residual: Optional[torch.Tensor] = None):
     """y = act(GroupNorm(x) [+ residual]); act SiLU (``silu``) or ReLU (``relu``)."""
-    lib = _lib.load()
-    _need(x, torch.bfloat16, "groupnorm x")
+    lib = _lib.load(act_dtype())
+    _need(x, act_dtype(), "groupnorm x")
     M = x.shape[0]
     C1 = x.shape[1]
     C = C1 + (x2.shape[1] if x2 is not None else 0)
     if out is None:
-        out = torch.empty((M, C), device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((M, C), device=x.device, dtype=act_dtype())
     ws_bytes = lib.acth_groupnorm_workspace_size(M, C, groups, rows_per_stat)
     ws = torch.empty((ws_bytes + 7) // 8, device=x.device, dtype=torch.float64)
     d = _lib.GroupNormDesc()
@@ -452,7 +479,7 @@ def groupnorm(x: torch.Tensor, gamma, beta, eps: float, rows_per_stat: int, *, x
         raise _lib.ActhError("groupnorm: silu and relu are exclusive")
     d.silu = 2 if relu else int(silu)
     if residual is not None:
-        _need(residual, torch.bfloat16, "groupnorm residual")
+        _need(residual, act_dtype(), "groupnorm residual")
         if residual.shape[0] < M or residual.shape[1] < C:
             raise _lib.ActhError(f"groupnorm: residual {tuple(residual.shape)} too small for ({M}, {C})")
         d.res, d.ldres = residual.data_ptr(), _rows(residual, "groupnorm residual")
@@ -464,9 +491,9 @@ def groupnorm(x: torch.Tensor, gamma, beta, eps: float, rows_per_stat: int, *, x
 
 def mamba_combine_ln(branch_a: dict, branch_e: dict, gamma, beta, eps: float, M: int, S: int, C: int, out=None):
     """Each branch dict: mode (0 none / 1 identity / 2 pos map), x, y0, y1, L, pos."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     if out is None:
-        out = torch.empty((M, C), device=gamma.device, dtype=torch.bfloat16)
+        out = torch.empty((M, C), device=gamma.device, dtype=act_dtype())
     d = _lib.MambaCombineDesc()
 
     def fill(pre, br):
@@ -498,18 +525,18 @@ SCAN_ALGO = int(os.environ.get("ACTH_SCAN_QUAD", "0"))
 
 def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks):
     """Checks and ScanDesc of one fused bidirectional scan; (None, y0, y1, None) when n_keep is 0."""
-    _need(u, torch.bfloat16, "scan u")
-    if xdbl.dtype not in (torch.float32, torch.bfloat16):
-        raise _lib.ActhError(f"scan xdbl must be float32 or bfloat16, got {xdbl.dtype}")
+    _need(u, act_dtype(), "scan u")
+    if xdbl.dtype not in (torch.float32, act_dtype()):
+        raise _lib.ActhError(f"scan xdbl must be float32 or {act_dtype()}, got {xdbl.dtype}")
     D = u.shape[1]
     for t, nm in ((dt_w, "dt_w"), (dt_b, "dt_b"), (A_log, "A_log"), (Dskip, "D")):
         _need(t, torch.float32, "scan " + nm)
         if not t.is_contiguous():
             raise _lib.ActhError(f"scan {nm} must be contiguous")
     if y0 is None:
-        y0 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
+        y0 = torch.empty((nb * n_keep, D), device=u.device, dtype=act_dtype())
     if y1 is None:
-        y1 = torch.empty((nb * n_keep, D), device=u.device, dtype=torch.bfloat16)
+        y1 = torch.empty((nb * n_keep, D), device=u.device, dtype=act_dtype())
     if n_keep == 0:
         return None, y0, y1, None
     d = _lib.ScanDesc()
@@ -519,7 +546,7 @@ def _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1
     d.y0, d.y1, d.ldy = y0.data_ptr(), y1.data_ptr(), _rows(y0, "scan y0")
     d.nb, d.L, d.D, d.R, d.N, d.n_keep = nb, L, D, R, 16, n_keep
     d.softplus, d.G, d.u_gstride, d.y_gstride, d.flip1 = 1, 2, 0, 0, 1
-    d.xdbl_bf16 = int(xdbl.dtype == torch.bfloat16)
+    d.xdbl_bf16 = int(xdbl.dtype == act_dtype())
     d.scan_algo = SCAN_ALGO
     if d.xdbl_bf16:
         d.nchunks = 1          # the bf16-xdbl kernel is single-pass
@@ -533,7 +560,7 @@ def selective_scan(u: torch.Tensor, xdbl: torch.Tensor, dt_w, dt_b, A_log, Dskip
     """Fused bidirectional scan. u: (nb*L, D) bf16; xdbl: (nb*L, 2*(R+32)) fp32 rows [dt | B | C] per
     direction, or bf16 rows (the reference's x_dbl dtype) of 2*(R4+32) with R4 = R rounded up to 4
     (dt padding columns ignored; ``SS2D_Unit.packed()['xproj_pad']`` holds the x_proj weights in that layout)."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     d, y0, y1, ws = _fused_scan_desc(u, xdbl, dt_w, dt_b, A_log, Dskip, nb, L, R, n_keep, y0, y1, nchunks)
     if d is not None:
         _lib.check(lib.acth_selective_scan(ctypes.byref(d), _stream()), "acth_selective_scan")
@@ -545,7 +572,7 @@ def selective_scan2(a: dict, b: dict):
     """Two fused bidirectional scans (selective_scan's keyword arguments each: u, xdbl, dt_w, dt_b,
     A_log, Dskip, nb, L, R, n_keep) in one launch -- SS2D_cond_v10's audio and expression branches.
     Returns ((y0, y1) of a, (y0, y1) of b)."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     da, ya0, ya1, wsa = _fused_scan_desc(nchunks=1, y0=None, y1=None, **a)
     db, yb0, yb1, wsb = _fused_scan_desc(nchunks=1, y0=None, y1=None, **b)
     if da is not None and db is not None:
@@ -567,7 +594,7 @@ def scan_auto_chunks(nb: int, G: int, D: int, L: int) -> int:
 
 
 def _scan_chunking(d, nb, G, D, L, nchunks, device):
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     nc = scan_auto_chunks(nb, G, D, L) if nchunks is None else int(nchunks)
     d.nchunks = nc
     ws = None
@@ -583,13 +610,13 @@ def selective_scan_op(u_t: torch.Tensor, delta_t: torch.Tensor, bc: torch.Tensor
                       G: int, softplus: bool, out: Optional[torch.Tensor] = None, nchunks: Optional[int] = None):
     """Generic op mode: u_t (nb*L, G*D) bf16, delta_t (nb*L, G*D) fp32/bf16, bc (nb*L, G*32) fp32
     [B(16) | C(16)] per group, forward traversal, all L outputs -> (nb*L, G*D) bf16."""
-    lib = _lib.load()
-    _need(u_t, torch.bfloat16, "scan u")
+    lib = _lib.load(act_dtype())
+    _need(u_t, act_dtype(), "scan u")
     _need(bc, torch.float32, "scan B/C")
     GD = u_t.shape[1]
     D = GD // G
     if out is None:
-        out = torch.empty((nb * L, GD), device=u_t.device, dtype=torch.bfloat16)
+        out = torch.empty((nb * L, GD), device=u_t.device, dtype=act_dtype())
     d = _lib.ScanDesc()
     d.u, d.ldu = u_t.data_ptr(), _rows(u_t, "scan u")
     d.xdbl, d.ldx = bc.data_ptr(), _rows(bc, "scan B/C")
@@ -610,22 +637,23 @@ def selective_scan_op(u_t: torch.Tensor, delta_t: torch.Tensor, bc: torch.Tensor
 # ------------------------------------------------------------------------------------------
 def timestep_embedding(t: torch.Tensor, dim: int, flip_sin_to_cos: bool = True, shift: float = 0.0,
                        scale: float = 1.0, max_period: float = 10000.0) -> torch.Tensor:
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     t = t.to(torch.float32).contiguous()
-    out = torch.empty((t.numel(), dim), device=t.device, dtype=torch.bfloat16)
+    out = torch.empty((t.numel(), dim), device=t.device, dtype=act_dtype())
     _lib.check(lib.acth_timestep_embedding(_p(t), t.numel(), dim, int(flip_sin_to_cos), shift, scale,
                                            max_period, _p(out), _stream()), "acth_timestep_embedding")
     return out
 
 
-def nchw_to_tokens(x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
+def nchw_to_tokens(x: torch.Tensor, out_dtype=None) -> torch.Tensor:
     """(B, C, H, W) or (B, F, C, H, W) -> (B*[F*]H*W, C)."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     x = x.contiguous()
     C, H, W = x.shape[-3:]
     B = x.numel() // (C * H * W)
-    if x.dtype not in (torch.float32, torch.bfloat16):
+    if x.dtype not in (torch.float32, act_dtype()):
         x = x.float()
+    out_dtype = act_dtype() if out_dtype is None else out_dtype
     out = torch.empty((B * H * W, C), device=x.device, dtype=out_dtype)
     _lib.check(lib.acth_nchw_to_tokens(_p(x), int(x.dtype == torch.float32), _p(out),
                                        int(out_dtype == torch.float32), C, B, C, H * W, _stream()),
@@ -634,7 +662,7 @@ def nchw_to_tokens(x: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
 
 
 def tokens_to_nchw(x: torch.Tensor, B: int, H: int, W: int, out_dtype=torch.float32) -> torch.Tensor:
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     C = x.shape[1]
     out = torch.empty((B, C, H, W), device=x.device, dtype=out_dtype)
     _lib.check(lib.acth_tokens_to_nchw(_p(x), int(x.dtype == torch.float32), _rows(x, "tokens"), _p(out),
@@ -644,10 +672,10 @@ def tokens_to_nchw(x: torch.Tensor, B: int, H: int, W: int, out_dtype=torch.floa
 
 
 def im2col3x3(x: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     C = x.shape[1]
     K = 9 * C
-    out = torch.empty((B * H * W, K), device=x.device, dtype=torch.bfloat16)
+    out = torch.empty((B * H * W, K), device=x.device, dtype=act_dtype())
     _lib.check(lib.acth_im2col3x3(_p(x.contiguous()), B, H, W, C, _p(out), K, _stream()), "acth_im2col3x3")
     return out
 
@@ -656,35 +684,35 @@ def im2col(x: torch.Tensor, B: int, H: int, W: int, kh: int, kw: int, stride: in
            kpad: Optional[int] = None) -> torch.Tensor:
     """NHWC rows (B*H*W, C) -> (B*Ho*Wo, Kpad) patches, column (ky*kw + kx)*C + c, zero-padded to Kpad
     (default: kh*kw*C rounded up to a multiple of 8)."""
-    lib = _lib.load()
-    _need(x, torch.bfloat16, "im2col x")
+    lib = _lib.load(act_dtype())
+    _need(x, act_dtype(), "im2col x")
     C = x.shape[1]
     if x.shape[0] != B * H * W:
         raise _lib.ActhError(f"im2col: x has {x.shape[0]} rows, expected {B * H * W}")
     Ho, Wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
     K = kh * kw * C
     kp = (K + 7) // 8 * 8 if kpad is None else kpad
-    out = torch.empty((B * Ho * Wo, kp), device=x.device, dtype=torch.bfloat16)
+    out = torch.empty((B * Ho * Wo, kp), device=x.device, dtype=act_dtype())
     _lib.check(lib.acth_im2col(_p(x), _rows(x, "im2col x"), B, H, W, C, kh, kw, stride, pad, Ho, Wo, _p(out), kp,
                                _stream()), "acth_im2col")
     return out
 
 
 def maxpool2d(x: torch.Tensor, B: int, H: int, W: int, k: int, stride: int, pad: int) -> torch.Tensor:
-    lib = _lib.load()
-    _need(x, torch.bfloat16, "maxpool x")
+    lib = _lib.load(act_dtype())
+    _need(x, act_dtype(), "maxpool x")
     C = x.shape[1]
     if x.shape[0] != B * H * W:
         raise _lib.ActhError(f"maxpool: x has {x.shape[0]} rows, expected {B * H * W}")
     Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
-    out = torch.empty((B * Ho * Wo, C), device=x.device, dtype=torch.bfloat16)
+    out = torch.empty((B * Ho * Wo, C), device=x.device, dtype=act_dtype())
     _lib.check(lib.acth_maxpool2d(_p(x), _rows(x, "maxpool x"), B, H, W, C, k, stride, pad, Ho, Wo, _p(out),
                                   _rows(out, "maxpool out"), _stream()), "acth_maxpool2d")
     return out
 
 
 def gather_rows(src: torch.Tensor, idx: torch.Tensor, nb: int, Ls: int, dst: torch.Tensor, Ld: int):
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     _need(idx, torch.int32, "gather idx")
     C = src.shape[1]
     _lib.check(lib.acth_gather_rows(_p(src), _rows(src, "gather src"), Ls, _p(idx), idx.numel(), _p(dst),
@@ -694,9 +722,9 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, nb: int, Ls: int, dst: tor
 
 def frame_mean(x: torch.Tensor, B: int, F: int, T: int) -> torch.Tensor:
     """x rows ((b*F + f)*T + t) -> rows (b*T + t), mean over f."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     C = x.shape[1]
-    out = torch.empty((B * T, C), device=x.device, dtype=torch.bfloat16)
+    out = torch.empty((B * T, C), device=x.device, dtype=act_dtype())
     _lib.check(lib.acth_frame_mean(_p(x), _rows(x, "frame_mean x"), B, F, T, C, _p(out), C, _stream()),
                "acth_frame_mean")
     return out
@@ -705,22 +733,22 @@ def frame_mean(x: torch.Tensor, B: int, F: int, T: int) -> torch.Tensor:
 def window_input(lat: torch.Tensor, frame_idx: torch.Tensor, img: torch.Tensor, branch: torch.Tensor,
                  in_scale: float, U: int, F: int, S: int, T: int) -> torch.Tensor:
     """lat (T*S, 4) fp32, img (nbranch*T*S, 4) fp32 -> (U*F*S, 8) bf16 UNet input."""
-    lib = _lib.load()
-    out = torch.empty((U * F * S, 8), device=lat.device, dtype=torch.bfloat16)
+    lib = _lib.load(act_dtype())
+    out = torch.empty((U * F * S, 8), device=lat.device, dtype=act_dtype())
     _lib.check(lib.acth_window_input(_p(lat), _p(frame_idx), _p(img), _p(branch), float(in_scale), _p(out),
                                      U, F, S, T, _stream()), "acth_window_input")
     return out
 
 
 def cfg_euler_accum(noise, unit_off, lat, frame_idx, g1, g2, g3, sigma, sigma_next, acc, cnt, F, S):
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     _lib.check(lib.acth_cfg_euler_accum(_p(noise), _p(unit_off), _p(lat), _p(frame_idx), float(g1), float(g2),
                                         float(g3), float(sigma), float(sigma_next), _p(acc), _p(cnt), F, S,
                                         _stream()), "acth_cfg_euler_accum")
 
 
 def div_counter(acc, cnt, out, T, S):
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     _lib.check(lib.acth_div_counter(_p(acc), _p(cnt), _p(out), T, S, _stream()), "acth_div_counter")
     return out
 
@@ -741,8 +769,8 @@ def conv_direct(x: torch.Tensor, wp: torch.Tensor, bias: Optional[torch.Tensor],
     """Direct 3x3 (pad 1, stride 1/2) or (3,1,1) temporal conv on NHWC rows for narrow channels.
     ``wp`` from :func:`pack_conv_direct`; ``temporal=dict(F, S)`` selects the frame-axis form; ``pad0``
     pads only bottom/right (diffusers Downsample2D with padding=0: F.pad(x, (0, 1, 0, 1)), conv pad 0)."""
-    lib = _lib.load()
-    _need(x, torch.bfloat16, "conv_direct x")
+    lib = _lib.load(act_dtype())
+    _need(x, act_dtype(), "conv_direct x")
     _need(wp, torch.float32, "conv_direct w")
     Cin = x.shape[1] if x.dim() == 2 else None
     taps = 3 if temporal is not None else 9
@@ -764,7 +792,7 @@ def conv_direct(x: torch.Tensor, wp: torch.Tensor, bias: Optional[torch.Tensor],
         d.mode, d.F, d.S = 1, Fr, S
         M = B * Fr * S
     if out is None:
-        out = torch.empty((M, Cout), device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        out = torch.empty((M, Cout), device=x.device, dtype=torch.float32 if out_f32 else act_dtype())
     d.x, d.ldx = x.data_ptr(), _rows(x, "conv_direct x")
     d.w = wp.data_ptr()
     if bias is not None:
@@ -778,11 +806,11 @@ def conv_direct(x: torch.Tensor, wp: torch.Tensor, bias: Optional[torch.Tensor],
 
 def softmax_rows(x: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 softmax(scale * x) over the last dim of an fp32 (rows, cols) matrix."""
-    lib = _lib.load()
+    lib = _lib.load(act_dtype())
     _need(x, torch.float32, "softmax x")
     rows, cols = x.shape
     if out is None:
-        out = torch.empty((rows, cols), device=x.device, dtype=torch.bfloat16)
+        out = torch.empty((rows, cols), device=x.device, dtype=act_dtype())
     _lib.check(lib.acth_softmax_rows(_p(x), _rows(x, "softmax x"), _p(out), _rows(out, "softmax out"), rows, cols,
                                      float(scale), _stream()), "acth_softmax_rows")
     return out

@@ -127,13 +127,17 @@ class HipBackend:
         # run the UNet prefix once per (window, prefix class) inside a call (LoopConfig.share_cfg_prefix)
         self.share_prefix = True
         nb = image_latents.shape[0]
+        # the UNet's activation dtype (bf16, or fp16 for an fp16 UNet: unet.compute_dtype())
+        cdt = unet.compute_dtype() if hasattr(unet, "compute_dtype") else torch.bfloat16
+        self.cdt = cdt
         # conditioning in device layouts, converted once per run
         self.img = ops.nchw_to_tokens(image_latents.to(dev).float(), out_dtype=torch.float32)     # (nb*T*S, 4)
-        self.ide = image_embeddings.to(dev, torch.bfloat16).reshape(nb, T, -1)                    # (nb, T, 1024)
-        self.aud = (audio_prompts.to(dev, torch.float32) * self.gate[0]).to(torch.bfloat16)        # (nb, T, 32, 1024)
+        self.ide = image_embeddings.to(dev, cdt).reshape(nb, T, -1)                               # (nb, T, 1024)
+        self.aud = (audio_prompts.to(dev, torch.float32) * self.gate[0]).to(cdt)                  # (nb, T, 32, 1024)
         self.n_audio = self.aud.shape[2]
-        self.vas = (vasa_prompts.to(dev, torch.float32) * self.gate[1]).to(torch.bfloat16).reshape(nb, T, -1)
-        self.pose = ops.nchw_to_tokens(pose_fea.to(dev))                                            # (P*S, 320)
+        self.vas = (vasa_prompts.to(dev, torch.float32) * self.gate[1]).to(cdt).reshape(nb, T, -1)
+        with ops.compute_dtype(cdt):
+            self.pose = ops.nchw_to_tokens(pose_fea.to(dev))                                        # (P*S, 320)
         # pose features may hold P != T frames (the pipeline's pose list has N frames): the reference
         # indexes them with the raw window index mod P (indice_slice, pipeline:687-693), not mod T
         self.pose_P = pose_fea.shape[1]
@@ -208,6 +212,10 @@ class HipBackend:
     def run_units(self, lat: torch.Tensor, units: Sequence[Tuple[int, int]], frames: List[List[int]],
                   t: float, sigma: float, out: torch.Tensor, row0: int):
         """UNet on ``units``; noise rows written to out[row0 : row0 + U*F*S]."""
+        with self.ops.compute_dtype(self.cdt):
+            self._run_units(lat, units, frames, t, sigma, out, row0)
+
+    def _run_units(self, lat, units, frames, t, sigma, out, row0):
         ops, F, S = self.ops, self.F, self.S
         U = len(units)
         fl_h = [f for (w, _c) in units for f in frames[w]]

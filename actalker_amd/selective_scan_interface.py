@@ -43,7 +43,7 @@ def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_
     A = A.float()
     if bool((A >= 0).any()):
         raise ValueError("selective_scan_fn (actalker_amd) expects A < 0 (A = -exp(A_log))")
-    u_t = u.transpose(1, 2).reshape(batch * L, dim).to(torch.bfloat16).contiguous()
+    u_t = u.transpose(1, 2).reshape(batch * L, dim).to(ops.act_dtype()).contiguous()
     d_t = delta.transpose(1, 2).reshape(batch * L, dim).float().contiguous()
     bc = torch.cat([B.float(), C.float()], dim=2)                    # (batch, G, 32, L)
     bc = bc.permute(0, 3, 1, 2).reshape(batch * L, G * 2 * N).contiguous()

@@ -290,12 +290,12 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             id_h, ip = encoder_hidden_states, None
         if id_h.shape[0] == B:
             id_h = id_h.repeat_interleave(F, dim=0)
-        ctx.id_tok = id_h.reshape(B * F, -1).to(dev, torch.bfloat16).contiguous()
+        ctx.id_tok = id_h.reshape(B * F, -1).to(dev, ops.act_dtype()).contiguous()
         if ip is not None:
             a, v = ip[0], ip[1]
             ctx.n_audio = a.shape[-2]
-            ctx.audio_tok = a.reshape(B * F * ctx.n_audio, -1).to(dev, torch.bfloat16).contiguous()
-            ctx.vasa_tok = v.reshape(B * F, -1).to(dev, torch.bfloat16).contiguous()
+            ctx.audio_tok = a.reshape(B * F * ctx.n_audio, -1).to(dev, ops.act_dtype()).contiguous()
+            ctx.vasa_tok = v.reshape(B * F, -1).to(dev, ops.act_dtype()).contiguous()
             ctx.audio_mean = ops.frame_mean(ctx.audio_tok, B, F, ctx.n_audio)
             ctx.vasa_mean = ops.frame_mean(ctx.vasa_tok, B, F, 1)
         else:
@@ -410,13 +410,24 @@ class UNetSpatioTemporalConditionModel(nn.Module):
                 ctx.vid[id(a)] = out[:, o:o + wt.shape[0]]
                 o += wt.shape[0]
 
+    def compute_dtype(self) -> torch.dtype:
+        """Activation dtype of the HIP path: ``acth_compute_dtype`` when set (torch.bfloat16 / torch.float16),
+        otherwise fp16 for a UNet whose weights are fp16 -- the dtype the reference runs its UNet in
+        (Inference.py:168-173, ``weight_dtype: fp16`` in its config) -- and bf16 for any other weight dtype.
+        Weights are packed per dtype (modules._pk), so both paths can run on one module tree."""
+        d = getattr(self, "acth_compute_dtype", None)
+        if d is None:
+            d = torch.float16 if self.conv_in.weight.dtype == torch.float16 else torch.bfloat16
+        return d
+
     def forward_tokens(self, x_tok: torch.Tensor, B: int, F: int, H: int, W: int, timestep, encoder_hidden_states,
                        added_time_ids, spatial_condition_tok: Optional[torch.Tensor] = None,
                        cross_attention_kwargs: Optional[Dict[str, Any]] = None,
                        spatial_condition_rmap: Optional[torch.Tensor] = None, out_f32: bool = True,
                        spatial_condition_rmap_max: Optional[int] = None,
                        prefix_src: Optional[Sequence[int]] = None):
-        """Token-major entry: x_tok (B*F*H*W, in_channels) bf16 -> (B*F*H*W, out_channels).
+        """Token-major entry: x_tok (B*F*H*W, in_channels) -> (B*F*H*W, out_channels), computed with
+        ``compute_dtype()`` activations (token inputs in another dtype are converted on entry).
         ``spatial_condition_rmap`` (device int32, one entry per frame) remaps frame rows of
         ``spatial_condition_tok``; ``spatial_condition_rmap_max`` is the host-side bound on its entries.
 
@@ -430,6 +441,19 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         if self.device.type != "cuda":
             raise RuntimeError("UNetSpatioTemporalConditionModel (actalker_amd) runs on the MI355X HIP kernels "
                                "only; move it to a GPU device first")
+        dt = self.compute_dtype()
+        with ops.compute_dtype(dt):
+            if x_tok.dtype != dt:
+                x_tok = x_tok.to(dt)
+            if spatial_condition_tok is not None and spatial_condition_tok.dtype != dt:
+                spatial_condition_tok = spatial_condition_tok.to(dt)
+            return self._forward_tokens(x_tok, B, F, H, W, timestep, encoder_hidden_states, added_time_ids,
+                                        spatial_condition_tok, cross_attention_kwargs, spatial_condition_rmap,
+                                        out_f32, spatial_condition_rmap_max, prefix_src)
+
+    def _forward_tokens(self, x_tok, B, F, H, W, timestep, encoder_hidden_states, added_time_ids,
+                        spatial_condition_tok, cross_attention_kwargs, spatial_condition_rmap, out_f32,
+                        spatial_condition_rmap_max, prefix_src):
         ctx = self._prep_ctx(B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs)
         S0 = H * W
         uniq = None
@@ -516,7 +540,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
                 cross_attention_kwargs: Optional[Dict[str, Any]] = None, return_dict: bool = True):
         B, F = sample.shape[:2]
         H, W = sample.shape[-2:]
-        with torch.no_grad():
+        with torch.no_grad(), ops.compute_dtype(self.compute_dtype()):
             x = ops.nchw_to_tokens(sample.to(self.device))
             sc = ops.nchw_to_tokens(spatial_condition.to(self.device)) if spatial_condition is not None else None
             out = self.forward_tokens(x, B, F, H, W, timestep, encoder_hidden_states, added_time_ids, sc,

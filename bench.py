@@ -35,7 +35,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
+PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense; fp16 is the same)
 PEAK_HBM_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s achievable)
 # algorithmic TFLOP per UNet frame-forward: (height, width, mode 2?)
 TFLOP_PER_FRAME_FWD = {(576, 1024, True): 3.433, (576, 1024, False): 3.402, (576, 576, False): 1.779}
@@ -427,6 +427,9 @@ def main():
                          "2 GiB buffer extents; the reference's call is 4 units = 56 frames)")
     ap.add_argument("--concurrent-calls", type=int, default=1,
                     help="run a rank's independent UNet calls of a step on this many HIP streams")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="activation dtype of the UNet kernels (fp16: libactalker_hip_f16.so, the reference's "
+                         "shipped weight_dtype)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -451,6 +454,7 @@ def main():
     unet_cpu = build_unet(dev)
     unet = unet_cpu.to(dev)
     unet.acth_batch_ctx_projections = not args.no_batch_ctx_proj
+    unet.acth_compute_dtype = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     if args.no_pair_scan:
         from actalker_amd import modules as _m
         for mod in unet.modules():
@@ -573,7 +577,7 @@ def main():
             "metric": "denoised frames/sec, 576x1024x14f x25-step audio-driven, 1/2/4/8 MI355X",
             "value": round(fps, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": f"{mode_name}, {H}x{W}, {N} frames ({args.frames_per_gpu}/GPU), fpb {fpb}, "
                                    f"25-step EulerDiscrete, 4-way CFG ({len(branches)} distinct branch inputs evaluated"
                                    + (f", branch {sorted(twins)} = twin {[twins[k] for k in sorted(twins)]} under gate "

@@ -17,8 +17,17 @@ def header_functions():
     return sorted(set(re.findall(r"^\s*(?:int|size_t)\s+(acth_\w+)\s*\(", src, flags=re.M)))
 
 
-def test_library_exports_every_declared_symbol():
-    lib = _lib.load()
+LIB_DTYPES = ["bf16", "fp16"]        # libactalker_hip.so and libactalker_hip_f16.so (ACTH_F16 build)
+
+
+def load(which):
+    import torch
+    return _lib.load(torch.float16 if which == "fp16" else torch.bfloat16)
+
+
+@pytest.mark.parametrize("which", LIB_DTYPES)
+def test_library_exports_every_declared_symbol(which):
+    lib = load(which)
     names = header_functions()
     assert len(names) >= 19
     for n in names:
@@ -27,8 +36,9 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(names)
 
 
-def test_struct_layouts_match_header():
-    lib = _lib.load()
+@pytest.mark.parametrize("which", LIB_DTYPES)
+def test_struct_layouts_match_header(which):
+    lib = load(which)
     assert lib.acth_gemm_desc_size() == ctypes.sizeof(_lib.GemmDesc)
     src = open(HEADER).read()
     for cname, py in (("ActhGemmDesc", _lib.GemmDesc), ("ActhAttnDesc", _lib.AttnDesc),
@@ -42,8 +52,9 @@ def test_struct_layouts_match_header():
         assert fields == [f[0] for f in py._fields_], cname
 
 
-def test_invalid_arguments_rejected_without_launch():
-    lib = _lib.load()
+@pytest.mark.parametrize("which", LIB_DTYPES)
+def test_invalid_arguments_rejected_without_launch(which):
+    lib = load(which)
     d = _lib.GemmDesc()
     assert lib.acth_gemm(ctypes.byref(d), None) == -1               # null operands
     d.A, d.B, d.C = 16, 16, 16
@@ -70,3 +81,19 @@ def test_no_cpu_fallback():
     from actalker_amd import ops
     with pytest.raises(_lib.ActhError):
         ops.layernorm(torch.zeros(4, 8, dtype=torch.bfloat16), None, None)
+
+
+def test_libraries_are_distinct_builds():
+    import torch
+    from actalker_amd import ops
+    assert _lib.load(torch.float16) is not _lib.load(torch.bfloat16)
+    assert ops.act_dtype() == torch.bfloat16
+    with ops.compute_dtype(torch.float16):
+        assert ops.act_dtype() == torch.float16
+        with ops.compute_dtype(torch.bfloat16):
+            assert ops.act_dtype() == torch.bfloat16
+        assert ops.act_dtype() == torch.float16
+    assert ops.act_dtype() == torch.bfloat16
+    with pytest.raises(_lib.ActhError):
+        with ops.compute_dtype(torch.float32):
+            pass

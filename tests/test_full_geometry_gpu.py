@@ -86,6 +86,33 @@ def test_unet_full_geometry_matches_oracle(dev, full_unet, case):
         assert st["rel_l2"] < 1.5 * st["bf16_rounding_rel_l2"], st
 
 
+@pytest.mark.parametrize("case", ["mode0", "half"])
+def test_unet_full_geometry_fp16_matches_fp16_budget(dev, full_unet, case):
+    """The fp16 activation path (libactalker_hip_f16.so, UNet.acth_compute_dtype = float16 -- what an fp16
+    UNet selects by itself, the reference's shipped weight_dtype, Inference.py:168-173) at 576x1024 against
+    the fp32 oracle. Stated tolerance: within 1.5x of the deviation the oracle itself shows when every op's
+    weights / inputs / outputs are rounded to fp16 (tests/golden/unet_full_*_rounded.safetensors "fp16",
+    tools/gen_golden_fp16.py) -- 1.6-1.8e-3, ~8x tighter than the bf16 bound above."""
+    unet, _ = full_unet
+    g = load_file(os.path.join(GOLD, f"unet_full_{case}.safetensors"))
+    rd = load_file(os.path.join(GOLD, f"unet_full_{case}_rounded.safetensors"))
+    sample, t, ehs, added, pose, masks = gf.case_inputs(case)
+    unet.acth_compute_dtype = torch.float16
+    try:
+        out = unet(sample.to(dev), t.to(dev), (ehs[0].to(dev), [e.to(dev) for e in ehs[1]]), added.to(dev),
+                   spatial_condition=pose.to(dev), cross_attention_kwargs={"ip_adapter_masks": masks},
+                   return_dict=False)[0]
+    finally:
+        unet.acth_compute_dtype = None
+    st = _stats(out, g["out"])
+    st["fp16_ref_path_rel_l2"] = _stats(rd["fp16"], g["out"])["rel_l2"]
+    st["vs_fp16_ref_path_rel_l2"] = _stats(out, rd["fp16"])["rel_l2"]
+    _log(f"unet_full_{case}_fp16", st)
+    assert torch.isfinite(out).all()
+    assert st["rel_l2"] < 1.5 * st["fp16_ref_path_rel_l2"], st
+    assert st["max_abs"] < 0.05 * st["ref_rms"], st
+
+
 # ------------------------------------------------------------------------------------------ scan
 def _bf(t):
     return t.to(torch.bfloat16)

@@ -1,7 +1,9 @@
-"""GPU: each libactalker_hip.so kernel against a plain torch fp32 computation of the same op.
+"""GPU: each kernel against a plain torch fp32 computation of the same op, in both builds: bf16 activations
+(libactalker_hip.so) and fp16 activations (libactalker_hip_f16.so, ops.compute_dtype) -- every test runs once
+per build (the ``act`` fixture).
 
-Inputs are rounded to bf16 first so the comparison measures only the kernel's accumulation and
-output rounding. Tolerance: relative L2 error <= 1e-2 (bf16 output, fp32 accumulation) unless
+Inputs are rounded to the activation dtype first so the comparison measures only the kernel's accumulation and
+output rounding. Tolerance: relative L2 error <= 1e-2 (16-bit output, fp32 accumulation) unless
 noted; the scan uses the oracle's restated mamba-ssm selective_scan_ref."""
 import math
 
@@ -16,7 +18,8 @@ pytestmark = pytest.mark.gpu
 
 
 def bf(x):
-    return x.to(torch.bfloat16)
+    """Round to the activation dtype of the build under test (bf16 or fp16)."""
+    return x.to(ops.act_dtype())
 
 
 def rel(a, b):
@@ -32,6 +35,12 @@ def rnd(*shape, scale=1.0, g=None):
 @pytest.fixture(autouse=True)
 def _seed():
     torch.manual_seed(1234)
+
+
+@pytest.fixture(autouse=True, params=["bf16", "fp16"])
+def act(request):
+    with ops.compute_dtype(torch.float16 if request.param == "fp16" else torch.bfloat16):
+        yield request.param
 
 
 # ------------------------------------------------------------------------------------------ GEMM
@@ -84,7 +93,7 @@ def test_gemm_geglu_and_orow(dev):
     assert out.shape == (M, inner)
     assert rel(out, h * F.gelu(g)) < 1e-2
     # orow: rows (m / 50) * 64 + m % 50 + 3 of a bigger buffer
-    buf = torch.zeros(4 * 64 + 8, 96, device=dev, dtype=torch.bfloat16)
+    buf = torch.zeros(4 * 64 + 8, 96, device=dev, dtype=ops.act_dtype())
     w3 = bf(rnd(96, C, scale=C ** -0.5))
     ops.gemm(x.to(dev), w3.to(dev), out=buf, orow=(50, 64, 3))
     refo = x.float() @ w3.float().t()
@@ -170,16 +179,16 @@ def test_geglu_ffn_fused_layernorm(dev, M, case):
 
 def test_geglu_ffn_rejects_bad_shapes(dev):
     from actalker_amd import _lib
-    x = torch.zeros(8, 640, device=dev, dtype=torch.bfloat16)
-    w1 = torch.zeros(8 * 640, 640, device=dev, dtype=torch.bfloat16)
-    w2 = torch.zeros(640, 4 * 640, device=dev, dtype=torch.bfloat16)
+    x = torch.zeros(8, 640, device=dev, dtype=ops.act_dtype())
+    w1 = torch.zeros(8 * 640, 640, device=dev, dtype=ops.act_dtype())
+    w2 = torch.zeros(640, 4 * 640, device=dev, dtype=ops.act_dtype())
     with pytest.raises(_lib.ActhError):
         ops.geglu_ffn(x, w1, None, w2, None)
-    x = torch.zeros(8, 320, device=dev, dtype=torch.bfloat16)
-    w1 = torch.zeros(8 * 320, 320, device=dev, dtype=torch.bfloat16)
-    w2 = torch.zeros(320, 4 * 320, device=dev, dtype=torch.bfloat16)
+    x = torch.zeros(8, 320, device=dev, dtype=ops.act_dtype())
+    w1 = torch.zeros(8 * 320, 320, device=dev, dtype=ops.act_dtype())
+    w2 = torch.zeros(320, 4 * 320, device=dev, dtype=ops.act_dtype())
     with pytest.raises(_lib.ActhError):
-        ops.geglu_ffn(x, w1, None, w2, None, residual=torch.zeros(4, 320, device=dev, dtype=torch.bfloat16))
+        ops.geglu_ffn(x, w1, None, w2, None, residual=torch.zeros(4, 320, device=dev, dtype=ops.act_dtype()))
 
 
 @pytest.mark.parametrize("tile", [4, 5])
@@ -264,7 +273,7 @@ def test_gemm_host_bounds_checks(dev):
         ops.gemm(a, w, residual=bf(rnd(200, 128)).to(dev), rmap=torch.tensor([0, 1, 2], dtype=torch.int32, device=dev),
                  r_div=100, r_mod=3, rmap_max=2)
     with pytest.raises(ActhError):
-        ops.gemm(a, w, out=torch.empty(300, 128, device=dev, dtype=torch.bfloat16), orow=(100, 110, 0))
+        ops.gemm(a, w, out=torch.empty(300, 128, device=dev, dtype=ops.act_dtype()), orow=(100, 110, 0))
 
 
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7])
@@ -380,11 +389,11 @@ def test_gemm_over_2gib(dev):
     from actalker_amd.modules import pack_conv3x3
     g = torch.Generator(device=dev).manual_seed(7)
     M, K, LDA, N, RB = 1_100_000, 1024, 2048, 128, 9216
-    big = torch.randn(M, LDA, device=dev, generator=g, dtype=torch.float32).to(torch.bfloat16)
+    big = torch.randn(M, LDA, device=dev, generator=g, dtype=torch.float32).to(ops.act_dtype())
     a = big[:, :K]                                   # 4.5 GB rows, 2.25 GB operand extent
-    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(ops.act_dtype())
     rowb = torch.randn(-(-M // RB), N, device=dev, generator=g)
-    res = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    res = torch.randn(M, N, device=dev, generator=g).to(ops.act_dtype())
     out = ops.gemm(a, w, rowbias=rowb, rb_div=RB, residual=res)
     chunk = ((1 << 30) - 65536) // (RB * LDA) * RB   # first chunk's rows (whole row-bias images)
     for r0 in (0, chunk - 700, chunk, M - 1000):
@@ -396,7 +405,7 @@ def test_gemm_over_2gib(dev):
     # slots, modules.SS2D_cond_v10): chunks are whole remap groups, C rebased by group
     OD, OS = 9216, 9249
     ngrp = -(-M // OD)
-    outr = torch.zeros(ngrp * OS, N, device=dev, dtype=torch.bfloat16)
+    outr = torch.zeros(ngrp * OS, N, device=dev, dtype=ops.act_dtype())
     ops.gemm(a, w, out=outr, orow=(OD, OS, 0))
     chunk = ((1 << 30) - 65536) // (OD * LDA) * OD
     for r0 in (0, chunk - 700, chunk, M - 1000):
@@ -409,8 +418,8 @@ def test_gemm_over_2gib(dev):
     torch.cuda.empty_cache()
     # conv: 190 images of 72 x 128 x 640 -> 2.24 GB of A
     B, H, W, Cin, Cout = 190, 72, 128, 640, 320
-    x = torch.randn(B * H * W, Cin, device=dev, generator=g).to(torch.bfloat16)
-    wc = (torch.randn(Cout, Cin, 3, 3, device=dev, generator=g) * (9 * Cin) ** -0.5).to(torch.bfloat16)
+    x = torch.randn(B * H * W, Cin, device=dev, generator=g).to(ops.act_dtype())
+    wc = (torch.randn(Cout, Cin, 3, 3, device=dev, generator=g) * (9 * Cin) ** -0.5).to(ops.act_dtype())
     out = ops.conv3x3(x, pack_conv3x3(wc), B, H, W)
     per = (1 << 30) // (H * W * Cin)                 # images per chunk
     for b in (0, per - 1, per, B - 1):
@@ -582,7 +591,7 @@ def test_layernorm_and_add(dev):
     out = ops.layernorm(x.to(dev), g.to(dev), b.to(dev), 1e-5)
     assert rel(out, F.layer_norm(x.float(), (C,), g, b, 1e-5)) < 1e-2
     add = bf(rnd(3, C))
-    s = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    s = torch.empty(M, C, device=dev, dtype=ops.act_dtype())
     out = ops.layernorm(x.to(dev), g.to(dev), b.to(dev), 1e-5, add=add.to(dev), add_div=100, sum_out=s)
     xs = bf(x.float() + add.float().repeat_interleave(100, 0)).float()
     assert rel(s, xs) < 5e-3
@@ -775,7 +784,7 @@ def test_layout_and_gather(dev):
     torch.testing.assert_close(back.cpu(), x.flatten(0, 1))
     src = bf(rnd(2 * 10, 16))
     idx = torch.tensor([9, 0, 4], dtype=torch.int32)
-    dst = torch.zeros(2 * 6, 16, device=dev, dtype=torch.bfloat16)
+    dst = torch.zeros(2 * 6, 16, device=dev, dtype=ops.act_dtype())
     ops.gather_rows(src.to(dev), idx.to(dev), 2, 10, dst, 6)
     got = dst.cpu().view(2, 6, 16)
     assert torch.equal(got[:, :3], src.view(2, 10, 16)[:, idx.long()])

@@ -386,7 +386,7 @@ def cpu_baseline(unet, H, W, frames=2, mode=0):
     d = got - want
     parity = dict(rel_l2=round((d.norm() / want.norm()).item(), 6), max_abs=round(d.abs().max().item(), 5),
                   ref_rms=round(want.pow(2).mean().sqrt().item(), 5), tol_rel_l2=2e-2,
-                  sample=f"HIP bf16 vs oracle fp32, one UNet call (1 CFG branch x {frames} frames, {H}x{W}, "
+                  sample=f"HIP {'fp16' if unet.compute_dtype() == torch.float16 else 'bf16'} vs oracle fp32, one UNet call (1 CFG branch x {frames} frames, {H}x{W}, "
                          f"mode {mode} masks / gated prompts), same weights and inputs")
     per_frame_fwd = dt / frames
     fps = 1.0 / (per_frame_fwd * 200.0)

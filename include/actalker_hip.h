@@ -13,6 +13,9 @@
  * Conventions (all entry points):
  *   - device pointers, caller-allocated; activations are token-major rows x channels, bf16
  *     (raw 16-bit) unless a field says fp32; weights are (out, in) row-major bf16;
+ *   - libactalker_hip_f16.so exports the same entry points built with fp16 activations (the
+ *     reference's shipped weight_dtype, config/inference.yaml:66): there every "bf16" operand
+ *     below is IEEE half; fp32 operands and all descriptors are unchanged;
  *   - stream-ordered on `stream`; no allocation, no host synchronisation (graph-capturable);
  *   - return ACTH_OK (0), ACTH_EINVAL (-1) for a rejected shape/alignment, or ACTH_ELAUNCH (-2)
  *     when the launch failed.

@@ -103,7 +103,7 @@ def main():
               os.path.join(ROOT, "tests", "golden", "c1_loop25_mode0.safetensors"))
     summary = {
         "workload": "C1: mode 0, 576x576 (latent 72x72), N = 14, fpb 14, 25 steps, 2 windows x 4 CFG branches "
-                    "(reference-shaped: no twin elimination), fp32 oracle (oracle/reference_cpu.py)",
+                    "(a branch whose window inputs are bitwise another branch's evaluated once), fp32 oracle (oracle/reference_cpu.py)",
         "unet_calls": len(log["calls"]), "frame_forwards": 14 * len(log["calls"]),
         "wall_seconds_loop": round(total, 1), "weight_build_seconds": round(t_build, 1),
         "threads": torch.get_num_threads(), "host": os.uname().nodename,

@@ -81,6 +81,40 @@ def unit_owner(n_windows: int, world: int, n_branch: int = 4,
     return owners
 
 
+def window_twins(frame_eq: Optional[torch.Tensor], frames: Sequence[int], global_twins: dict) -> dict:
+    """{branch: earlier branch} for one window: branch c reads branch e's noise prediction when their UNet inputs are
+    bitwise equal on every frame of the window (``frame_eq[c, e, f]``, HipBackend.frame_equal). Besides the
+    run-wide twins (mode 0: "cond" = "drop vasa"), this finds the windows that lie wholly in the fpb padding frames
+    past N: there every CFG branch but the unconditional one carries the same ID embedding and image latents and
+    the same uncond audio / VASA pad (pipeline:175-184), so branches 2 and 3 are branch 1's twins in every mode.
+    ``frame_eq`` None: the run-wide twins only."""
+    if frame_eq is None:
+        return dict(global_twins)
+    twins = {}
+    idx = torch.as_tensor(list(frames), dtype=torch.long)
+    for c in range(1, frame_eq.shape[0]):
+        for e in range(c):
+            if e not in twins and bool(frame_eq[c, e, idx].all()):
+                twins[c] = e
+                break
+    return twins
+
+
+def step_units(n_windows: int, twins_per_window: Sequence[dict], n_branch: int = 4) -> List[Tuple[int, int]]:
+    """The (window, branch) units a step evaluates, window-major: every branch that is not a twin in its window."""
+    return [(w, c) for w in range(n_windows) for c in range(n_branch) if c not in twins_per_window[w]]
+
+
+def split_units(units: Sequence[Tuple[int, int]], world: int, rank: int) -> Tuple[List[Tuple[int, int]], int]:
+    """Contiguous block of ``units`` for ``rank`` and the per-rank capacity (the all-gather slot count)."""
+    n = len(units)
+    cap = math.ceil(n / world)
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    count = base + (1 if rank < extra else 0)
+    return list(units[start:start + count]), cap
+
+
 def call_splits(n_units: int, max_per_call: int) -> List[Tuple[int, int]]:
     """[start, end) unit ranges: the fewest UNet calls of at most ``max_per_call`` units, sizes
     differing by at most one (5 units, max 4 -> 3 + 2 rather than 4 + 1)."""
@@ -192,6 +226,27 @@ class HipBackend:
                     twins[c] = e
                     break
         return twins
+
+    def frame_equal(self) -> torch.Tensor:
+        """(nb, nb, T) bool on the host: [c, e, f] = CFG branches c and e receive bitwise-equal UNet inputs at latent
+        frame f -- ID embedding, image latents, gated audio and VASA prompts of that frame, and the added time ids
+        (the window's noisy latents, timestep, pose rows and masks are shared by construction). A window whose frames
+        are all equal for (c, e) has c's noise prediction = e's (every kernel is deterministic and the UNet treats
+        batch elements independently), so c is read from e's rows (pipeline.window_twins)."""
+        if getattr(self, "_frame_eq", None) is None:
+            nb, T = self.ide.shape[0], self.T
+            img = self.img.reshape(nb, T, -1)
+            eq = torch.zeros((nb, nb, T), dtype=torch.bool)
+            for c in range(nb):
+                for e in range(c):
+                    if not torch.equal(self.added[c], self.added[e]):
+                        continue
+                    m = ((img[c] == img[e]).all(-1) & (self.ide[c] == self.ide[e]).reshape(T, -1).all(-1)
+                         & (self.aud[c] == self.aud[e]).reshape(T, -1).all(-1)
+                         & (self.vas[c] == self.vas[e]).reshape(T, -1).all(-1))
+                    eq[c, e] = m.cpu()
+            self._frame_eq = eq
+        return self._frame_eq
 
     def begin_step(self, raw_frames: List[List[int]]):
         self._raw = raw_frames
@@ -305,11 +360,14 @@ class LoopConfig:
 
 
 def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, world: int = 1,
-            group=None, step_callback: Optional[Callable[[int], None]] = None, steps: Optional[int] = None):
+            group=None, step_callback: Optional[Callable[[int], None]] = None, steps: Optional[int] = None,
+            plan_log: Optional[list] = None):
     """Run the sampler loop. ``latents_all``: (1, T, 4, h, w) (already ``add_noise``d, pipeline:586-598).
 
     With world > 1, torch.distributed must be initialised; each rank runs its unit block and one
-    ``all_gather_into_tensor`` per step exchanges the noise predictions."""
+    ``all_gather_into_tensor`` per step exchanges the noise predictions. The units are planned per step
+    (window_twins: which CFG branches of each window have another branch's inputs); ``plan_log``, when given,
+    receives one {units, rank_units} entry per step."""
     T = cfg.num_frames + cfg.frames_per_batch
     F = cfg.frames_per_batch
     sigmas, timesteps = karras_sigmas(cfg.num_inference_steps, cfg.sigma_min, cfg.sigma_max)
@@ -321,32 +379,53 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
         broadcast_from_rank0(lat, group)
     n_windows = len(range(0, T, F - cfg.overlap))
     twins = backend.branch_twins() if (cfg.dedup_branches and hasattr(backend, "branch_twins")) else {}
+    frame_eq = backend.frame_equal() if (cfg.dedup_branches and hasattr(backend, "frame_equal")) else None
+    if frame_eq is not None and world > 1:
+        # every rank must plan the same units (the all-gather sizes depend on them): a pair of branches counts as
+        # equal at a frame only if it is equal on every rank
+        import torch.distributed as dist
+        flags = frame_eq.to(torch.int32)
+        if dist.get_backend(group) == "nccl":
+            flags = flags.to(lat.device)
+        dist.all_reduce(flags, op=dist.ReduceOp.MIN, group=group)
+        frame_eq = flags.cpu().bool()
     if hasattr(backend, "share_prefix"):
         backend.share_prefix = cfg.share_cfg_prefix
-    branches = [c for c in range(4) if c not in twins]
-    my_units, cap = assign_units(n_windows, world, rank, branches=branches)
-    owners = unit_owner(n_windows, world, branches=branches)
     S = backend.S
     rows_per_unit = F * S
-    local = torch.zeros((cap * rows_per_unit, 4), device=lat.device, dtype=torch.float32)
-    gathered = torch.empty((world * cap * rows_per_unit, 4), device=lat.device, dtype=torch.float32) \
+    cap_max = math.ceil(n_windows * 4 / world)
+    local = torch.zeros((cap_max * rows_per_unit, 4), device=lat.device, dtype=torch.float32)
+    gathered = torch.empty((world * cap_max * rows_per_unit, 4), device=lat.device, dtype=torch.float32) \
         if world > 1 else local
-    # row offset of every global unit inside the gathered buffer
-    unit_row = [(r * cap + slot) * rows_per_unit for (r, slot) in owners]
     shift = 0
     n_steps = cfg.num_inference_steps if steps is None else steps
     upc = cfg.units_per_call
     if upc <= 0:
         upc = backend.max_units_per_call() if hasattr(backend, "max_units_per_call") else 4
-    calls = call_splits(len(my_units), upc)
     streams = []
-    if cfg.concurrent_calls > 1 and len(calls) > 1 and lat.is_cuda:
-        streams = [torch.cuda.Stream(device=lat.device) for _ in range(min(cfg.concurrent_calls, len(calls)))]
     for i in range(n_steps):
         frames = window_frames(T, F, cfg.overlap, shift)
+        # this step's units: per window, the CFG branches whose inputs are not another branch's (window_twins)
+        tw = [window_twins(frame_eq, frames[w], twins) for w in range(n_windows)]
+        units = step_units(n_windows, tw)
+        my_units, cap = split_units(units, world, rank)
+        if plan_log is not None:
+            plan_log.append(dict(units=len(units), rank_units=len(my_units)))
+        index = {u: k for k, u in enumerate(units)}
+        base, extra = divmod(len(units), world)
+        # row offset of global unit k inside the gathered buffer: rank r's block starts at r * cap units
+        owner_row = []
+        for r in range(world):
+            cnt = base + (1 if r < extra else 0)
+            owner_row += [(r * cap + slot) * rows_per_unit for slot in range(cnt)]
+        calls = call_splits(len(my_units), upc)
+        if cfg.concurrent_calls > 1 and len(calls) > 1 and lat.is_cuda and len(streams) < min(cfg.concurrent_calls,
+                                                                                               len(calls)):
+            streams += [torch.cuda.Stream(device=lat.device)
+                        for _ in range(min(cfg.concurrent_calls, len(calls)) - len(streams))]
         if hasattr(backend, "begin_step"):
             backend.begin_step(window_frames_raw(T, F, cfg.overlap, shift))
-        if streams:
+        if streams and len(calls) > 1:
             main = torch.cuda.current_stream(lat.device)
             for s in streams:
                 s.wait_stream(main)                  # this step's latent state is ready
@@ -362,9 +441,9 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
                 backend.run_units(lat, chunk, frames, timesteps[i], sigmas[i], local, c0 * rows_per_unit)
         if world > 1:
             import torch.distributed as dist
-            dist.all_gather_into_tensor(gathered, local, group=group)
-        pos = {c: branches.index(twins.get(c, c)) for c in range(4)}
-        unit_rows = [[unit_row[w * len(branches) + pos[c]] for c in range(4)] for w in range(n_windows)]
+            n = cap * rows_per_unit
+            dist.all_gather_into_tensor(gathered[:world * n], local[:n], group=group)
+        unit_rows = [[owner_row[index[(w, tw[w].get(c, c))]] for c in range(4)] for w in range(n_windows)]
         g = cfg.guidance if cfg.guidance_schedule is None else cfg.guidance_schedule[i]
         lat = backend.step_windows(lat, gathered, unit_rows, frames, g, sigmas[i], sigmas[i + 1])
         shift = (shift + cfg.shift_offset) % F

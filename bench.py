@@ -8,8 +8,11 @@ A "step" is one sampler step of the loop (pipeline:671): every window x CFG-bran
 (one 84-frame call in modes 0/1, two 56-frame calls in mode 2, at N=14 on one GPU) + guidance + Euler + window accumulation. In modes 0 / 1 the
 gate zeroes the VASA / audio prompts (pipeline:724), so two of the four CFG branches receive
 bitwise-identical inputs; that branch is evaluated once and read twice by guidance (identical
-output; pipeline.HipBackend.branch_twins), i.e. 3 x 14-frame UNet batches per window. --no-dedup
-evaluates all four, as the reference does. The sampler's
+output; pipeline.HipBackend.branch_twins), i.e. 3 x 14-frame UNet batches per window. In every mode, a
+window lying wholly in the fpb padding frames past N (every other step at N = 14, shift 7) gives branches
+1-3 the same inputs -- the same ID embedding and image latents and the uncond audio / VASA pad for all
+branches (pipeline:175-184) -- so there branches 2 and 3 read branch 1's prediction
+(pipeline.window_twins). --no-dedup evaluates all four everywhere, as the reference does. The sampler's
 steps are shape-identical, so frames/sec = N_frames / (25 * seconds_per_step). Weak scaling: each GPU
 adds 14 output frames (N = 14 * world), units = (window, CFG branch) sharded contiguously, one RCCL
 all-gather of noise predictions per step.
@@ -485,8 +488,9 @@ def main():
     ftimer = None if args.no_roofline else FamilyTimer().install()
     barrier()
     t_start = time.perf_counter()
+    plan = []
     with torch.no_grad():
-        out = pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.steps)
+        out = pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.steps, plan_log=plan)
     barrier()
     elapsed = time.perf_counter() - t_start
     if timer is not None:
@@ -525,11 +529,12 @@ def main():
                 time_frac=round(rt, 4), hbm_bound_time_share=round(hbm_share, 4),
                 definition="sum over GEMM launches of max(FLOP / 2500 TFLOP/s, algorithmic bytes / 8000 GB/s) "
                            "divided by the sum of measured launch times")
-    n_units_rank = len(pl.assign_units(len(range(0, N + fpb, fpb)), world, rank, branches=branches)[0])
-    frame_fwds = n_units_rank * fpb * args.steps
+    frame_fwds = sum(p["rank_units"] for p in plan) * fpb
+    n_windows = len(range(0, N + fpb, fpb))
+    units_per_step = sum(p["units"] for p in plan) / max(1, len(plan))
     # the reference-shaped figure: all four CFG branches evaluated (no twin-branch elimination), same steps
     four = None
-    if twins and world == 1 and not args.no_four_branch_compare:
+    if cfg.dedup_branches and world == 1 and not args.no_four_branch_compare:
         cfg4 = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=7,
                              concurrent_calls=args.concurrent_calls, dedup_branches=False,
                              units_per_call=args.units_per_call, share_cfg_prefix=False)
@@ -561,13 +566,16 @@ def main():
                 pl.denoise(be_m, inp_m["latents"], cfg, rank, world, group, steps=1)
             barrier()
             tm = time.perf_counter()
+            plan_m = []
             with torch.no_grad():
-                out_m = pl.denoise(be_m, inp_m["latents"], cfg, rank, world, group, steps=args.steps)
+                out_m = pl.denoise(be_m, inp_m["latents"], cfg, rank, world, group, steps=args.steps, plan_log=plan_m)
             barrier()
             em = time.perf_counter() - tm
             other[f"mode{m}"] = dict(workload=name_m, value=round(N / (cfg.num_inference_steps * em / args.steps), 4),
                                      ms_per_step=round(1000.0 * em / args.steps, 2), steps=args.steps,
-                                     cfg_branches_evaluated=4 - len(tw_m), finite=bool(torch.isfinite(out_m).all()))
+                                     cfg_branches_evaluated=4 - len(tw_m),
+                                     units_per_step=round(sum(p["units"] for p in plan_m) / max(1, len(plan_m)), 2),
+                                     finite=bool(torch.isfinite(out_m).all()))
             del be_m, inp_m, out_m
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -582,13 +590,16 @@ def main():
                                    f"25-step EulerDiscrete, 4-way CFG ({len(branches)} distinct branch inputs evaluated"
                                    + (f", branch {sorted(twins)} = twin {[twins[k] for k in sorted(twins)]} under gate "
                                       f"{gate}" if twins else "")
-                                   + f"), (window x branch) units over {world} GPU(s)",
+                                   + f"; padding-only windows: branches 2, 3 = twin 1; {units_per_step:.2f} of "
+                                     f"{4 * n_windows} (window x branch) units per step evaluated), units over "
+                                     f"{world} GPU(s)",
                        "model": "SVD-XT UNet + ACTalker v10 dual-Mamba (1.775B, random init)",
                        "global_batch": N, "seq_len": fpb, "parallelism": f"units{world}"},
             "unet_frame_forwards_per_s_per_gpu": round(frame_fwds / elapsed, 3),
             "achieved_mfma_tflops_whole_step": (round(frame_fwds * TFLOP_PER_FRAME_FWD[(H, W, args.mode == 2)] / elapsed, 1)
                                                 if (H, W, args.mode == 2) in TFLOP_PER_FRAME_FWD else None),
             "cfg_branches_evaluated": len(branches),
+            "units_per_step": {"evaluated": round(units_per_step, 2), "reference": 4 * n_windows},
             "cfg_prefix_shared": cfg.share_cfg_prefix,
             "all_four_branches": four,
             "other_modes": other,

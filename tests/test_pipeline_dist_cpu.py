@@ -86,6 +86,35 @@ class TwinCpuBackend(CpuBackend):
         return {3: 2}
 
 
+class PadTwinCpuBackend(CpuBackend):
+    """The pipeline's padding structure (pipeline:175-184): past frame N every CFG branch but the unconditional one
+    carries the same conditioning, so in a window made only of padding frames branches 2 and 3 have branch 1's
+    inputs. The stand-in UNet sees a per-(branch, frame) condition code instead of the branch id, so equal inputs
+    give equal outputs, and the backend reports the per-frame input equality (HipBackend.frame_equal)."""
+
+    def __init__(self, image_latents, h, w, T, fpb, N):
+        super().__init__(image_latents, h, w, T, fpb)
+        self.cond = torch.arange(4, dtype=torch.float32)[:, None].repeat(1, T)
+        self.cond[1:, N:] = 1.0
+        self.img[2:, N:] = self.img[1, N:]
+
+    def run_units(self, lat, units, frames, t, sigma, out, row0):
+        F, S = self.F, self.S
+        for u, (wdx, c) in enumerate(units):
+            idx = frames[wdx]
+            x = torch.cat([lat[0, idx] / math.sqrt(sigma * sigma + 1.0), self.img[c, idx]], dim=1)
+            noise = fake_unet(x + self.cond[c, idx].view(-1, 1, 1, 1), 0, t)
+            out[row0 + u * F * S: row0 + (u + 1) * F * S] = noise.permute(0, 2, 3, 1).reshape(-1, 4)
+
+    def frame_equal(self):
+        nb, T = 4, self.T
+        eq = torch.zeros(nb, nb, T, dtype=torch.bool)
+        for c in range(nb):
+            for e in range(c):
+                eq[c, e] = (self.img[c] == self.img[e]).reshape(T, -1).all(-1) & (self.cond[c] == self.cond[e])
+        return eq
+
+
 def oracle_loop(latents, imgl, N, fpb, shift_offset, steps):
     sig, ts = ref.euler_karras_tables(25)
     T = N + fpb
@@ -125,7 +154,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, N, fpb, steps, q, twin=False):
+def _worker(rank, world, port, N, fpb, steps, q, twin=False, pad=False, shift=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -133,8 +162,11 @@ def _worker(rank, world, port, N, fpb, steps, q, twin=False):
         latents, imgl = make_case(N, fpb)
         if twin:
             imgl[3] = imgl[2]
-        backend = (TwinCpuBackend if twin else CpuBackend)(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
-        cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1, units_per_call=2)
+        if pad:
+            backend = PadTwinCpuBackend(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb, N)
+        else:
+            backend = (TwinCpuBackend if twin else CpuBackend)(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
+        cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=shift, units_per_call=2)
         out = pl.denoise(backend, latents, cfg, rank, world, steps=steps)
         q.put((rank, out))
     finally:
@@ -241,6 +273,66 @@ def test_twin_branch_evaluated_once_matches_four_branch_loop(world):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        torch.testing.assert_close(outs[r], want, rtol=0, atol=0)
+
+
+def test_window_twins_and_step_units():
+    T, N = 6, 3
+    eq = torch.zeros(4, 4, T, dtype=torch.bool)
+    eq[3, 2] = True                                     # run-wide twin (mode 0)
+    eq[2, 1, N:] = eq[3, 1, N:] = True                  # padding frames: branches 1-3 equal
+    assert pl.window_twins(eq, [0, 1, 2], {}) == {3: 2}
+    assert pl.window_twins(eq, [3, 4, 5], {}) == {2: 1, 3: 1}
+    assert pl.window_twins(eq, [2, 3, 4], {}) == {3: 2}          # mixed window
+    assert pl.window_twins(None, [3, 4, 5], {3: 2}) == {3: 2}    # no per-frame table: run-wide twins only
+    tw = [pl.window_twins(eq, f, {}) for f in ([0, 1, 2], [3, 4, 5])]
+    assert pl.step_units(2, tw) == [(0, 0), (0, 1), (0, 2), (1, 0), (1, 1)]
+    units = pl.step_units(2, tw)
+    got = [pl.split_units(units, 2, r) for r in range(2)]
+    assert got == [([(0, 0), (0, 1), (0, 2)], 3), ([(1, 0), (1, 1)], 3)]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_padding_window_twins_match_four_branch_loop(world):
+    """Per-window twins (a padding-only window evaluates branches 0 and 1; 2 and 3 read branch 1's rows) == all
+    four branches evaluated everywhere, bit for bit, on 1 process and on 2 gloo ranks. N = 6, fpb = 3, shift 1: the
+    padding window [6, 7, 8] occurs every third step."""
+    N, fpb, steps = 6, 3, 6
+    latents, imgl = make_case(N, fpb)
+    calls = []
+
+    class Counting(PadTwinCpuBackend):
+        def run_units(self, lat, units, frames, t, sigma, out, row0):
+            calls.extend(units)
+            super().run_units(lat, units, frames, t, sigma, out, row0)
+
+    b4 = Counting(imgl.clone(), latents.shape[3], latents.shape[4], N + fpb, fpb, N)
+    want = pl.denoise(b4, latents, pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1,
+                                                 units_per_call=2, dedup_branches=False), steps=steps)
+    assert len(calls) == 3 * 4 * steps
+    calls.clear()
+    if world == 1:
+        plan = []
+        got = pl.denoise(Counting(imgl.clone(), latents.shape[3], latents.shape[4], N + fpb, fpb, N), latents,
+                         pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1, units_per_call=2),
+                         steps=steps, plan_log=plan)
+        # shift 0 at steps 0 and 3: windows [0,1,2] [3,4,5] [6,7,8] -> the last is padding-only (2 units, not 4)
+        assert [p["units"] for p in plan] == [10, 12, 12, 10, 12, 12]
+        assert len(calls) == sum(p["units"] for p in plan)
+        assert torch.equal(got, want)
+        return
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q, False, True))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs = dict(q.get(timeout=300) for _ in range(world))

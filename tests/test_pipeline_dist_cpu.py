@@ -299,12 +299,13 @@ def test_window_twins_and_step_units():
     assert got == [([(0, 0), (0, 1), (0, 2)], 3), ([(1, 0), (1, 1)], 3)]
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_padding_window_twins_match_four_branch_loop(world):
+@pytest.mark.parametrize("world,N,fpb", [(1, 6, 3), (2, 6, 3), (8, 16, 2)])
+def test_padding_window_twins_match_four_branch_loop(world, N, fpb):
     """Per-window twins (a padding-only window evaluates branches 0 and 1; 2 and 3 read branch 1's rows) == all
-    four branches evaluated everywhere, bit for bit, on 1 process and on 2 gloo ranks. N = 6, fpb = 3, shift 1: the
-    padding window [6, 7, 8] occurs every third step."""
-    N, fpb, steps = 6, 3, 6
+    four branches evaluated everywhere, bit for bit, on 1 process and on 2 and 8 gloo ranks. N = 6, fpb = 3,
+    shift 1: the padding window [6, 7, 8] occurs every third step. World 8 at N = 16, fpb = 2 has C5's 9 windows:
+    36 units dealt 5,5,5,5,4,4,4,4 on the odd steps and 34 units dealt 5,5,4,4,4,4,4,4 on the even ones."""
+    steps = 6
     latents, imgl = make_case(N, fpb)
     calls = []
 
@@ -316,7 +317,7 @@ def test_padding_window_twins_match_four_branch_loop(world):
     b4 = Counting(imgl.clone(), latents.shape[3], latents.shape[4], N + fpb, fpb, N)
     want = pl.denoise(b4, latents, pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=1,
                                                  units_per_call=2, dedup_branches=False), steps=steps)
-    assert len(calls) == 3 * 4 * steps
+    assert len(calls) == len(range(0, N + fpb, fpb)) * 4 * steps
     calls.clear()
     if world == 1:
         plan = []
@@ -331,6 +332,9 @@ def test_padding_window_twins_match_four_branch_loop(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    if world == 8:
+        units = [pl.step_units(9, [{2: 1, 3: 1} if w == 8 else {} for w in range(9)])]
+        assert [len(pl.split_units(units[0], 8, r)[0]) for r in range(8)] == [5, 5, 4, 4, 4, 4, 4, 4]
     procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q, False, True))
              for r in range(world)]
     for p in procs:

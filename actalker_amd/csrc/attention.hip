@@ -730,8 +730,13 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
 //   O^T = V^T P^T  v_mfma_f32_16x16x16bf16_1k x 4 (d tiles): B = P^T is the score accumulator
 //                itself (as bf16), A = V^T from a per-wave LDS transpose of the V tile.
 // (A thread-per-query VALU kernel spent ~1000 VALU wave-instructions per tuple against ~60 here; both
-// are bound by the frame-strided row reads, ~2.5 TB/s at the level-0 shape, tools/bench_attn.py.)
-#define TM_TPW 4                 // tuples per wave (consecutive: heads of one row segment)
+// are bound by the frame-strided row reads: 4.1-4.5 TB/s at the level-0..2 shapes, tools/bench_attn.py.)
+// Tuples per wave (consecutive: heads of one row segment), all loads issued before the first use. Measured
+// (profiles/r4_step8_temporal_attn_tpw.log, B = 4 CFG branches): 2 -> 4.50 / 4.29 / 4.13 TB/s at S = 9216 / 2304 /
+// 576, 4 -> 4.45 / 4.11 / 3.94, 8 -> 3.59 / 3.41 / 3.36 (VGPRs for 8 tuples of loads cut the waves per SIMD).
+#ifndef TM_TPW
+#define TM_TPW 2
+#endif
 #define TM_VLD 20                // V^T LDS row: 16 keys + pad (40 B, 8-B aligned reads)
 
 __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTemporalAttnDesc p) {

@@ -9,7 +9,7 @@
 //                        query column: row max / row sum stay lane-local (+1 lane^32 exchange),
 //                        and S^T's accumulator registers feed the P.V product directly as the
 //                        B operand (O^T = V^T P^T), so no LDS round trip for P.
-//  * acth_temporal_attn: self-attention over the F (<=16) frames of a window at every spatial
+//  * acth_temporal_attn: self-attention over the F (<=32) frames of a window at every spatial
 //                        position (TemporalBasicTransformerBlock.attn1, attention.py:446-448).
 //  * acth_ip_attn      : IP-adapter cross attention (IPAdapterAttnProcessor2_0,
 //                        attention_processor.py:2747-2934). 1-key attentions (ID, VASA) are
@@ -722,121 +722,155 @@ extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
 // Temporal self-attention over frames. qkv rows are tokens (b, f, s) = (b*F + f)*S + s with
 // [q | k | v] column blocks of width C = H*64. Output o rows use the same token order.
 
-// One wave per (b, s, head) tuple at a time, the F <= 16 frames padded to
-// one 16 x 16 tile. Per tuple a lane issues 6 16-byte loads and the wave 6 MFMAs:
-//   S^T = K Q^T  v_mfma_f32_16x16x32_bf16 x 2: A = K, B = Q^T, both loaded as 16-B row chunks
-//                (lane l -> frame l % 16, dims 32 ks + 8 (l / 16)); lane l then holds the scores of
-//                keys 4 (l / 16) + i for query l % 16, so the softmax is in-lane + xor 16 / 32.
-//   O^T = V^T P^T  v_mfma_f32_16x16x16bf16_1k x 4 (d tiles): B = P^T is the score accumulator
-//                itself (as bf16), A = V^T from a per-wave LDS transpose of the V tile.
+// One wave per (b, s, head) tuple at a time, the F <= 16 NB frames padded to NB 16-frame blocks (NB = 1:
+// F <= 16, the 14-frame windows of the benched workload; NB = 2: F <= 32, the reference's shipped
+// n_sample_frames = 25 window, config/inference.yaml:4 -> Inference.py:573). Per tuple a lane issues 6 NB
+// 16-byte loads (frames fr + 16 blk) and the wave 2 NB^2 + 4 NB^2 MFMAs:
+//   S^T = K Q^T  v_mfma_f32_16x16x32_bf16 x 2 per (key block kb, query block qb): A = K, B = Q^T, both
+//                loaded as 16-B row chunks (lane l -> frame 16 blk + l % 16, dims 32 ks + 8 (l / 16)); lane l
+//                then holds the scores of keys 16 kb + 4 (l / 16) + i for query 16 qb + l % 16, so the softmax
+//                is in-lane (over kb, i) + xor 16 / 32.
+//   O^T = V^T P^T  v_mfma_f32_16x16x16bf16_1k x 4 (d tiles) x NB (query blocks) x NB (key blocks, accumulated):
+//                B = P^T is the score accumulator itself (as bf16), A = V^T from a per-wave LDS transpose.
 // (A thread-per-query VALU kernel spent ~1000 VALU wave-instructions per tuple against ~60 here; both
 // are bound by the frame-strided row reads: 4.1-4.5 TB/s at the level-0..2 shapes, tools/bench_attn.py.)
 // Tuples per wave (consecutive: heads of one row segment), all loads issued before the first use. Measured
-// (profiles/r4_step8_temporal_attn_tpw.log, B = 4 CFG branches): 2 -> 4.50 / 4.29 / 4.13 TB/s at S = 9216 / 2304 /
-// 576, 4 -> 4.45 / 4.11 / 3.94, 8 -> 3.59 / 3.41 / 3.36 (VGPRs for 8 tuples of loads cut the waves per SIMD).
+// at NB = 1 (profiles/r4_step8_temporal_attn_tpw.log, B = 4 CFG branches): 2 -> 4.50 / 4.29 / 4.13 TB/s at
+// S = 9216 / 2304 / 576, 4 -> 4.45 / 4.11 / 3.94, 8 -> 3.59 / 3.41 / 3.36 (VGPRs for 8 tuples of loads cut the
+// waves per SIMD). NB = 2 keeps the same bytes in flight per wave with one tuple.
 #ifndef TM_TPW
 #define TM_TPW 2
 #endif
-#define TM_VLD 20                // V^T LDS row: 16 keys + pad (40 B, 8-B aligned reads)
 
+template <int NB, int TPW>
 __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTemporalAttnDesc p) {
-  __shared__ __attribute__((aligned(16))) bf16_t vts[4][64 * TM_VLD];
+  constexpr int VLD = 16 * NB + 4;        // V^T LDS row: 16 NB keys + pad (8-B aligned reads)
+  __shared__ __attribute__((aligned(16))) bf16_t vts[4][64 * VLD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
   const long long ntup = (long long)p.B * p.S * p.H;
   const int C = p.H * 64;
   const float c = p.scale * 1.4426950408889634f;
   bf16_t* vt = vts[wave];
-  const bool fok = fr < p.F;
-  // every load of the wave's TM_TPW tuples is issued before the first is used (one latency per
+  bool fok[NB];
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) fok[blk] = 16 * blk + fr < p.F;
+  // every load of the wave's TPW tuples is issued before the first is used (one latency per
   // wave instead of one per tuple: the rows of a tuple are S rows apart, 64 B per lane group)
   const uint4 z = make_uint4(0, 0, 0, 0);
-  uint4 qa[TM_TPW][2], ka[TM_TPW][2], va[TM_TPW][2];
-  size_t rows[TM_TPW];
-  int heads[TM_TPW];
-  const long long tp0 = ((long long)blockIdx.x * 4 + wave) * TM_TPW;
+  uint4 qa[TPW][NB][2], ka[TPW][NB][2], va[TPW][NB][2];
+  size_t rows[TPW][NB];
+  int heads[TPW];
+  const long long tp0 = ((long long)blockIdx.x * 4 + wave) * TPW;
 #pragma unroll
-  for (int it = 0; it < TM_TPW; ++it) {
+  for (int it = 0; it < TPW; ++it) {
     const long long tp = tp0 + it < ntup ? tp0 + it : ntup - 1;
     const int h = (int)(tp % p.H);
     const long long bs = tp / p.H;
     const int s = (int)(bs % p.S), b = (int)(bs / p.S);
-    rows[it] = ((size_t)b * p.F + (fok ? fr : 0)) * p.S + s;           // frame fr of this tuple
     heads[it] = h;
-    const bf16_t* base = (const bf16_t*)p.qkv + rows[it] * p.ldqkv + h * 64 + 8 * g;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      qa[it][ks] = z; ka[it][ks] = z; va[it][ks] = z;      // guarded loads, not `fok ? *p : z`
-      if (fok) {                                           // (that form went through a stack slot)
-        qa[it][ks] = *reinterpret_cast<const uint4*>(base + 32 * ks);
-        ka[it][ks] = *reinterpret_cast<const uint4*>(base + C + 32 * ks);
-        va[it][ks] = *reinterpret_cast<const uint4*>(base + 2 * C + 32 * ks);
+    for (int blk = 0; blk < NB; ++blk) {
+      rows[it][blk] = ((size_t)b * p.F + (fok[blk] ? 16 * blk + fr : 0)) * p.S + s;   // frame 16 blk + fr
+      const bf16_t* base = (const bf16_t*)p.qkv + rows[it][blk] * p.ldqkv + h * 64 + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qa[it][blk][ks] = z; ka[it][blk][ks] = z; va[it][blk][ks] = z;   // guarded loads, not `fok ? *p : z`
+        if (fok[blk]) {                                                  // (that form went through a stack slot)
+          qa[it][blk][ks] = *reinterpret_cast<const uint4*>(base + 32 * ks);
+          ka[it][blk][ks] = *reinterpret_cast<const uint4*>(base + C + 32 * ks);
+          va[it][blk][ks] = *reinterpret_cast<const uint4*>(base + 2 * C + 32 * ks);
+        }
       }
     }
   }
 #pragma unroll
-  for (int it = 0; it < TM_TPW; ++it) {
+  for (int it = 0; it < TPW; ++it) {
     if (tp0 + it >= ntup) break;
-    const size_t row = rows[it];
     const int h = heads[it];
-    const uint4* qv = qa[it];
-    const uint4* kv = ka[it];
-    const uint4* vv = va[it];
-    // V^T[d][key] (lane holds V[key fr][d = 32 ks + 8 g + e]); the previous tuple's reads of vt
+    // V^T[d][key] (lane holds V[key 16 blk + fr][d = 32 ks + 8 g + e]); the previous tuple's reads of vt
     // were issued earlier by this wave, and a wave's LDS operations complete in order
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint32_t w4[4] = {vv[ks].x, vv[ks].y, vv[ks].z, vv[ks].w};
+    for (int blk = 0; blk < NB; ++blk)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        vt[(32 * ks + 8 * g + e) * TM_VLD + fr] = (bf16_t)(e & 1 ? w4[e >> 1] >> 16 : w4[e >> 1] & 0xffffu);
-    }
-    f32x4_t st = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint4 vv = va[it][blk][ks];
+        const uint32_t w4[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      st = mfma16x16x32(*reinterpret_cast<const bf16x8_t*>(&kv[ks]),
-                                                   *reinterpret_cast<const bf16x8_t*>(&qv[ks]), st);
-    // softmax over the keys of query fr: keys 4 g + i here, the other 12 in lanes fr + 16 k
-    float sc[4], mx = -INFINITY;
+        for (int e = 0; e < 8; ++e)
+          vt[(32 * ks + 8 * g + e) * VLD + 16 * blk + fr] =
+              (bf16_t)(e & 1 ? w4[e >> 1] >> 16 : w4[e >> 1] & 0xffffu);
+      }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      sc[i] = (4 * g + i < p.F) ? st[i] * c : -INFINITY;
-      mx = fmaxf(mx, sc[i]);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float pr[4], sum = 0.0f;
+    for (int qb = 0; qb < NB; ++qb) {
+      f32x4_t st[NB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      pr[i] = __builtin_amdgcn_exp2f(sc[i] - mx);
-      sum += pr[i];
-    }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = 1.0f / sum;
-    // P^T as the B operand: element j = key 4 g + j of query fr
-    const short4_t pb = __builtin_bit_cast(short4_t, make_uint2(pack2(pr[0], pr[1]), pack2(pr[2], pr[3])));
-    bf16_t* orow = (bf16_t*)p.o + row * p.ldo + h * 64 + 4 * g;
+      for (int kb = 0; kb < NB; ++kb) {
+        st[kb] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const short4_t a = *reinterpret_cast<const short4_t*>(&vt[(16 * dt + fr) * TM_VLD + 4 * g]);
-      const f32x4_t o = mfma16x16x16_s4(a, pb, f32x4_t{0.0f, 0.0f, 0.0f, 0.0f});
-      // o[i] = O[query fr][d = 16 dt + 4 g + i]
-      if (fok)
-        *reinterpret_cast<uint2*>(orow + 16 * dt) =
-            make_uint2(pack2(o[0] * inv, o[1] * inv), pack2(o[2] * inv, o[3] * inv));
+        for (int ks = 0; ks < 2; ++ks)
+          st[kb] = mfma16x16x32(*reinterpret_cast<const bf16x8_t*>(&ka[it][kb][ks]),
+                                *reinterpret_cast<const bf16x8_t*>(&qa[it][qb][ks]), st[kb]);
+      }
+      // softmax over the keys of query 16 qb + fr: keys 16 kb + 4 g + i here, the rest in lanes fr + 16 k
+      float sc[NB][4], mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[kb][i] = (16 * kb + 4 * g + i < p.F) ? st[kb][i] * c : -INFINITY;
+          mx = fmaxf(mx, sc[kb][i]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float sum = 0.0f;
+      short4_t pb[NB];
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        float pr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pr[i] = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
+          sum += pr[i];
+        }
+        // P^T as the B operand: element j = key 16 kb + 4 g + j of query 16 qb + fr
+        pb[kb] = __builtin_bit_cast(short4_t, make_uint2(pack2(pr[0], pr[1]), pack2(pr[2], pr[3])));
+      }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      const float inv = 1.0f / sum;
+      bf16_t* orow = (bf16_t*)p.o + rows[it][qb] * p.ldo + h * 64 + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f32x4_t o = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int kb = 0; kb < NB; ++kb) {
+          const short4_t a = *reinterpret_cast<const short4_t*>(&vt[(16 * dt + fr) * VLD + 16 * kb + 4 * g]);
+          o = mfma16x16x16_s4(a, pb[kb], o);
+        }
+        // o[i] = O[query 16 qb + fr][d = 16 dt + 4 g + i]
+        if (fok[qb])
+          *reinterpret_cast<uint2*>(orow + 16 * dt) =
+              make_uint2(pack2(o[0] * inv, o[1] * inv), pack2(o[2] * inv, o[3] * inv));
+      }
     }
   }
 }
 
 extern "C" int acth_temporal_attn(const ActhTemporalAttnDesc* d, hipStream_t stream) {
   if (!d || !d->qkv || !d->o) return ACTH_EINVAL;
-  if (d->F <= 0 || d->F > 16 || d->B <= 0 || d->S <= 0 || d->H <= 0) return ACTH_EINVAL;
+  if (d->F <= 0 || d->F > 32 || d->B <= 0 || d->S <= 0 || d->H <= 0) return ACTH_EINVAL;
   if (d->ldqkv % 8 || d->ldo % 8) return ACTH_EINVAL;
   const long long ntup = (long long)d->B * d->S * d->H;
-  const long long nblk = (ntup + 4 * TM_TPW - 1) / (4 * TM_TPW);
-  if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
-  hipLaunchKernelGGL(temporal_attn_mfma_kernel, dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  if (d->F <= 16) {
+    const long long nblk = (ntup + 4 * TM_TPW - 1) / (4 * TM_TPW);
+    if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
+    hipLaunchKernelGGL((temporal_attn_mfma_kernel<1, TM_TPW>), dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  } else {
+    const long long nblk = (ntup + 3) / 4;
+    if (nblk > 0x7fffffffLL) return ACTH_EINVAL;
+    hipLaunchKernelGGL((temporal_attn_mfma_kernel<2, 1>), dim3((unsigned)nblk), dim3(256), 0, stream, *d);
+  }
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

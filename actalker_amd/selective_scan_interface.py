@@ -14,9 +14,15 @@ A) raise NotImplementedError instead of silently differing.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
+
+# ACTH_CHECK_ARGS=1: validate A's sign on the host (a device -> host sync per call; off by default so the op keeps
+# the boundary's no-sync contract, include/actalker_hip.h)
+_CHECK_A = os.environ.get("ACTH_CHECK_ARGS", "0") == "1"
 
 
 def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_softplus=False,
@@ -41,8 +47,12 @@ def selective_scan_fn(u, delta, A, B, C, D=None, z=None, delta_bias=None, delta_
     if dim % G:
         raise ValueError("dim must be a multiple of the number of B/C groups")
     A = A.float()
-    if bool((A >= 0).any()):
-        raise ValueError("selective_scan_fn (actalker_amd) expects A < 0 (A = -exp(A_log))")
+    if _CHECK_A or not A.is_cuda:
+        # a device-side A would make this a host sync per call (30 per UNet forward); it is checked only on
+        # request. Unchecked, A > 0 puts NaN into every output of its channel (log of a negative value) and
+        # A = 0 is exact (log 0 = -inf, -exp(-inf) = 0): an invalid A is loud, never silently different.
+        if bool((A > 0).any()):
+            raise ValueError("selective_scan_fn (actalker_amd) expects A <= 0 (A = -exp(A_log))")
     u_t = u.transpose(1, 2).reshape(batch * L, dim).to(ops.act_dtype()).contiguous()
     d_t = delta.transpose(1, 2).reshape(batch * L, dim).float().contiguous()
     bc = torch.cat([B.float(), C.float()], dim=2)                    # (batch, G, 32, L)

@@ -95,8 +95,9 @@ typedef struct ActhAttnDesc {
 } ActhAttnDesc;
 int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream);
 
-/* ---- temporal self-attention over F <= 16 frames (TemporalBasicTransformerBlock.attn1,
- * attention.py:446-448) on fused [q|k|v] rows ordered (b, f, s) */
+/* ---- temporal self-attention over F <= 32 frames (TemporalBasicTransformerBlock.attn1,
+ * attention.py:446-448) on fused [q|k|v] rows ordered (b, f, s); F <= 32 covers the reference's shipped
+ * n_sample_frames = 25 window (config/inference.yaml:4 -> Inference.py:573 frames_per_batch) */
 typedef struct ActhTemporalAttnDesc {
   const void* qkv; int ldqkv; void* o; int ldo;
   int B, F, S, H;

@@ -27,13 +27,29 @@ H_PX, W_PX = 128, 256
 H, W = H_PX // 8, W_PX // 8
 STEPS = 25
 # per case: (gate, overlap, shift_offset); mode1 runs overlapping windows (accumulate / average, :748-756)
-CASES = {"mode0": ([1, 0], 0, 1), "mode1": ([0, 1], 1, 1), "mode2": ([1, 1], 0, 1)}
+CASES = {"mode0": ([1, 0], 0, 1), "mode1": ([0, 1], 1, 1), "mode2": ([1, 1], 0, 1),
+         # the reference's shipped window: frames_per_batch = n_sample_frames = 25 (config/inference.yaml:4,
+         # Inference.py:573) with its shipped shift_offset 7 / overlap 0 (inference.yaml); latent 8x16
+         "f25_mode0": ([1, 0], 0, 7), "f25_mode2": ([1, 1], 0, 7)}
+# per case geometry (N, fpb, H_PX, W_PX); the f25 cases run 2 windows of 25 frames (T = N + fpb = 29)
+GEOMETRY = {"f25_mode0": (4, 25, 64, 128), "f25_mode2": (4, 25, 64, 128)}
 GUIDANCE = dict(min_guidance_scale1=1.0, max_guidance_scale1=3.0, min_guidance_scale2=2.0, max_guidance_scale2=7.5,
                 min_guidance_scale3=1.5, max_guidance_scale3=3.0)
 CALL = dict(height=H_PX, width=W_PX, num_frames=N, num_inference_steps=STEPS, fps=12.5, motion_bucket_id=12,
             motion_bucket_id_exp=20, noise_aug_strength=0.02, frames_per_batch=FPB, i2i_noise_strength=1.0,
             **GUIDANCE)
 INPUT_SEED, GEN_SEED = 41, 7
+
+
+def geometry(case=None):
+    """(N, fpb, H_PX, W_PX) of ``case`` (the module defaults for the N = 4, fpb = 2 cases)."""
+    return GEOMETRY.get(case, (N, FPB, H_PX, W_PX))
+
+
+def call_kwargs(case=None):
+    """The __call__ keyword arguments of ``case`` besides the inputs, generator, overlap, shift and gate."""
+    n, fpb, hp, wp = geometry(case)
+    return dict(CALL, height=hp, width=wp, num_frames=n, frames_per_batch=fpb)
 
 
 class _StandIn(nn.Module):
@@ -89,11 +105,13 @@ class StandInPoseGuider(_StandIn):
         return torch.einsum("oc,bcnhw->bonhw", self.w, z)
 
 
-def raw_inputs(seed: int = INPUT_SEED):
+def raw_inputs(seed: int = INPUT_SEED, case=None):
     """The __call__ arguments the caller (Inference.py:547-577) hands the pipeline, synthetic and seeded:
     ref / clip images, N pose images (binary face boxes moving 8 px per frame: pose[0][0] is the face mask,
     :622), N expression (upper half) and mouth (lower half) mask images, N audio / uncond audio prompts
     (32, 1024), N VASA / uncond VASA prompts (1024,), and the initial noise ``latents`` (1, N + fpb, 4, h, w)."""
+    N, FPB, H_PX, W_PX = geometry(case)
+    H, W = H_PX // 8, W_PX // 8
     g = torch.Generator().manual_seed(seed)
     ref = torch.rand(1, 3, H_PX, W_PX, generator=g) * 2 - 1
     clip = torch.rand(1, 3, 224, 224, generator=g)
@@ -127,11 +145,12 @@ def standins(pose_channels: int):
     return StandInVAE(), StandInIDProj(), StandInPoseGuider(pose_channels)
 
 
-def oracle_loop_inputs(raw, vae, id_proj, pose_guider, gate):
+def oracle_loop_inputs(raw, vae, id_proj, pose_guider, gate, case=None):
     """Restatement of pipeline:128-205 (CFG stacking, uncond pads), :518-598 (ref / image latents, add_noise at
     sigma_max with the generator's noise-augmentation draw first), :600-638 (masks, pose features) and :640-657
     (per-step guidance) -> the arguments of oracle.reference_cpu.denoise_loop."""
     from oracle.reference_cpu import euler_karras_tables
+    N, FPB, _, _ = geometry(case)
     T = N + FPB
     ide = id_proj(raw["clip_image"]).unsqueeze(1).repeat(1, T, 1, 1)
     ide = torch.cat([torch.zeros_like(ide), ide, ide, ide])
@@ -176,9 +195,11 @@ def oracle_pipeline_loop(case: str, dtype=None):
         sd = precision.round_state_dict(sd, dtype)
         ctx = precision.rounded(dtype)
     gate, overlap, shift = CASES[case]
+    N, FPB, _, _ = geometry(case)
     vae, idp, pg = standins(gu.TINY_CFG["block_out_channels"][0])
     with torch.no_grad():
-        lat, imgl, ide, aud, vas, pose, added, masks, gs = oracle_loop_inputs(raw_inputs(), vae, idp, pg, gate)
+        lat, imgl, ide, aud, vas, pose, added, masks, gs = oracle_loop_inputs(raw_inputs(case=case), vae, idp, pg,
+                                                                              gate, case)
 
         def unet_fn(sample, t, ehs, added_ids, sc, cak):
             return ref.unet_forward(sd, sample, t, ehs, added_ids, sc, cak, ip_scale=(1.25, 1.25),

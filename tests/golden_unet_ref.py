@@ -7,6 +7,9 @@ The fixtures pin the reference's orchestration -- unet_spatio_temporal_condition
 :1394-1553 / 1902-1986 -- executed unchanged; only the diffusers 0.29.2 leaves (oracle/diffusers_leaves.py)
 and mamba-ssm's selective_scan_ref are restatements.
 
+* ``tiny_f25_half`` / ``tiny_f25_mode2``: the same tiny UNet at the reference's shipped window, F = 25 frames
+  (config/inference.yaml:4 -> Inference.py:573), B = 2; the temporal attention then spans two 16-frame MFMA
+  blocks (acth_temporal_attn's F <= 32 instantiation).
 * ``tiny_*``: the full UNet topology (4 down / mid / 4 up blocks, 15 v10 transformers with Mamba, IP
   adapters) at widths 64/128/128/128, heads 1/2/2/2, B = 2 CFG branches x F = 3 frames, latent 16x32
   (128x256 px masks). Mask cases follow the pipeline's gates (pipeline:702-711): mode0 [face, 0] with
@@ -31,7 +34,10 @@ TINY_CFG = dict(block_out_channels=(64, 128, 128, 128), num_attention_heads=(1, 
                 layers_per_block=2, num_frames=3)
 TINY_SEED = 5
 TINY_B, TINY_F, TINY_H, TINY_W = 2, 3, 16, 32
-TINY_CASES = ("tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box")
+TINY_CASES = ("tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box", "tiny_f25_half", "tiny_f25_mode2")
+# the reference's shipped window: config/inference.yaml:4 n_sample_frames = 25 -> Inference.py:573 frames_per_batch,
+# so every temporal block (attention.py:431-433, the temporal ResBlocks' (3,1,1) convs and GroupNorm) spans 25 frames
+F25 = 25
 FULL_CASES = ("full_half", "full_mode0", "full_mode2", "c1_face0")
 CASES = TINY_CASES + FULL_CASES
 SIGMA = 1.6555  # Karras step 12 of 25; t = 0.25 ln sigma
@@ -40,6 +46,9 @@ SIGMA = 1.6555  # Karras step 12 of 25; t = 0.25 ln sigma
 def tiny_inputs(case: str, seed: int = 23):
     g = torch.Generator().manual_seed(seed)
     B, F, h, w = TINY_B, TINY_F, TINY_H, TINY_W
+    if case.startswith("tiny_f25_"):
+        F = F25
+        case = "tiny_" + case[len("tiny_f25_"):]
     sample = torch.randn(B, F, 8, h, w, generator=g)
     t = torch.tensor(0.25 * math.log(SIGMA))
     ide = torch.randn(B * F, 1, 1024, generator=g)

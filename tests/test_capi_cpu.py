@@ -65,7 +65,7 @@ def test_invalid_arguments_rejected_without_launch(which):
     s.N, s.R, s.L, s.D, s.nb, s.G, s.ldx, s.ldu = 8, 4, 10, 64, 1, 2, 128, 64       # N != 16
     assert lib.acth_selective_scan(ctypes.byref(s), None) == -1
     a = _lib.TemporalAttnDesc()
-    a.qkv, a.o, a.F, a.B, a.S, a.H = 16, 16, 17, 1, 1, 1                   # F > 16
+    a.qkv, a.o, a.F, a.B, a.S, a.H = 16, 16, 33, 1, 1, 1                   # F > 32
     assert lib.acth_temporal_attn(ctypes.byref(a), None) == -1
     c = _lib.ConvDirectDesc()
     c.x, c.w, c.y, c.Cin, c.Cout, c.ldx, c.ldy, c.B, c.H, c.W, c.Ho, c.Wo = 16, 16, 16, 3, 16, 3, 16, 1, 8, 8, 8, 8

@@ -280,8 +280,8 @@ def test_c1_loop_matches_cpu_oracle(dev, full_unet, act):
 
 
 # ------------------------------------------------------------------------------------------ reference run
-@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box", "full_half",
-                                  "full_mode0", "full_mode2", "c1_face0"])
+@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box", "tiny_f25_half",
+                                  "tiny_f25_mode2", "full_half", "full_mode0", "full_mode2", "c1_face0"])
 def test_unet_matches_reference_run(dev, request, case):
     """HIP UNet forward against the REFERENCE UNet package's own forward (v10:362-517 and everything under it,
     run unchanged on the CPU by tools/gen_golden_unet_ref.py; only the diffusers leaves and the scan math
@@ -312,7 +312,7 @@ def test_unet_matches_reference_run(dev, request, case):
 
 # ------------------------------------------------------------------------------------------ reference sampler run
 @pytest.mark.parametrize("act", ["bf16", "fp16"])
-@pytest.mark.parametrize("case", ["mode0", "mode1", "mode2"])
+@pytest.mark.parametrize("case", ["mode0", "mode1", "mode2", "f25_mode0", "f25_mode2"])
 def test_pipeline_call_matches_reference_pipeline_run(dev, case, act):
     """The product Pose2VideoLongSVDPipeline.__call__ (actalker_amd/pipeline_svd.py: CFG stacking, add_noise,
     masks / pose plumbing, per-step guidance, the HIP loop) against the REFERENCE pipeline's own __call__
@@ -321,7 +321,8 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case, act):
     same deterministic VAE / ID-projection / pose-guider stand-ins (tests/golden_pipeline.py). Stated tolerance:
     within 1.5x of the deviation the bf16-rounded oracle version of the same run accumulates over the 25 steps
     (tools/gen_golden_pipeline_floor.py; the per-step guidance here reaches 7.5, so the rounding floor is higher
-    than the constant-guidance loop's), and below 5e-2. ``act`` fp16: the UNet with fp16 activations (the reference's
+    than the constant-guidance loop's), and below 5e-2. ``f25_*``: the reference's shipped window, frames_per_batch =
+    n_sample_frames = 25 (config/inference.yaml:4 -> Inference.py:573) with shift_offset 7, at a 8x16 latent. ``act`` fp16: the UNet with fp16 activations (the reference's
     shipped weight_dtype) held to 1.5x the fp16-rounded oracle run's deviation (``latents_fp16``) when present."""
     from actalker_amd.pipeline_svd import Pose2VideoLongSVDPipeline
     from tests import golden_pipeline as gp
@@ -338,10 +339,10 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case, act):
     pipe = Pose2VideoLongSVDPipeline(vae, unet, idp, pg).to(dev)
     if act == "fp16":
         unet.acth_compute_dtype = torch.float16
-    raw = gp.raw_inputs()
+    raw = gp.raw_inputs(case=case)
     with torch.no_grad():
         got = pipe(**raw, generator=torch.Generator().manual_seed(gp.GEN_SEED), output_type="latent",
-                   return_dict=False, overlap=overlap, shift_offset=shift, gate=gate, **gp.CALL)
+                   return_dict=False, overlap=overlap, shift_offset=shift, gate=gate, **gp.call_kwargs(case))
     st = _stats(got, g["latents"])
     tol = 3e-2
     fpath = os.path.join(GOLD, f"pipeline_floor_{case}.safetensors")

@@ -139,7 +139,7 @@ def test_oracle_attention_matches_reference_processor_golden(name):
 # the oracle's whole UNet forward against the REFERENCE UNet package run on the CPU
 # (tools/gen_golden_unet_ref.py: v10 UNet / unet_3d_blocks / TransformerSTmodel / attention /
 # attention_processor / mamba_layer executed unchanged, diffusers leaves = oracle/diffusers_leaves.py)
-@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box"])
+@pytest.mark.parametrize("case", ["tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box", "tiny_f25_half"])
 def test_oracle_unet_matches_reference_run(case):
     from tests import golden_full as gf
     from tests import golden_unet_ref as gu
@@ -219,7 +219,7 @@ def _pipeline_fixtures(case):
     return load_file(rpath), load_file(fpath)
 
 
-@pytest.mark.parametrize("case", ["mode0", "mode1", "mode2"])
+@pytest.mark.parametrize("case", ["mode0", "mode1", "mode2", "f25_mode0", "f25_mode2"])
 def test_oracle_loop_fixture_matches_reference_pipeline_run(case):
     """The oracle's version of each reference pipeline run (tests/golden_pipeline.oracle_pipeline_loop: the
     test-side restatement of the pipeline's stacking / plumbing -- CFG stacking and uncond pads, add_noise, masks

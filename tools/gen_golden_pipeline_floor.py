@@ -45,4 +45,4 @@ if __name__ == "__main__":
         i = args.index("--only")
         names = {args[i + 1]}
         args = args[:i] + args[i + 2:]
-    main(args or list(gp.CASES), names)
+    main(args or [c for c in gp.CASES if c not in gp.GEOMETRY], names)

@@ -141,11 +141,11 @@ def main(cases):
     sig, ts = euler_karras_tables(gp.STEPS)
     for case in cases:
         gate, overlap, shift = gp.CASES[case]
-        raw = gp.raw_inputs()
+        raw = gp.raw_inputs(case=case)
         t0 = time.time()
         out = pipe(**{k: (list(v) if isinstance(v, list) else v) for k, v in raw.items()},
                    generator=torch.Generator().manual_seed(gp.GEN_SEED), output_type="latent", return_dict=False,
-                   overlap=overlap, shift_offset=shift, gate=gate, **gp.CALL)
+                   overlap=overlap, shift_offset=shift, gate=gate, **gp.call_kwargs(case))
         print(f"{case}: reference __call__ {time.time() - t0:.0f}s, latents {tuple(out.shape)} "
               f"rms {out.pow(2).mean().sqrt():.4f}", flush=True)
         save_file({"latents": out.contiguous().float(), "weights_checksum": wsum, "inputs_checksum": gp.inputs_checksum(raw)},
@@ -153,4 +153,4 @@ def main(cases):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(gp.CASES))
+    main(sys.argv[1:] or [c for c in gp.CASES if c not in gp.GEOMETRY])

@@ -223,6 +223,7 @@ SIGNATURES = {
                               c_int, c_int, c_vp], c_int),
     "acth_div_counter": ([c_vp, c_vp, c_vp, c_int, c_int, c_vp], c_int),
     "acth_version": ([], c_int),
+    "acth_act_dtype": ([], c_int),
 }
 
 _libs = {}
@@ -250,6 +251,11 @@ def load(dtype=None):
         fn.restype = restype
     if lib.acth_gemm_desc_size() != ctypes.sizeof(GemmDesc):
         raise ActhError("ActhGemmDesc layout mismatch between include/actalker_hip.h and _lib.py")
+    if lib.acth_act_dtype() != int(f16):
+        # both libraries export the same ABI: a bf16 build loaded for fp16 (or the reverse, e.g. a stale
+        # ACTH_LIB_F16) would reinterpret every activation's bits
+        raise ActhError(f"{path} was built for {'fp16' if lib.acth_act_dtype() else 'bf16'} activations, "
+                        f"loaded for {'fp16' if f16 else 'bf16'}")
     _libs[f16] = lib
     return lib
 

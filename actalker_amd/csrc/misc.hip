@@ -322,3 +322,6 @@ extern "C" int acth_div_counter(const float* acc, const float* cnt, float* out, 
 }
 
 extern "C" int acth_version(void) { return 1; }
+
+// the activation dtype this library was compiled for (common.h ACTH_F16): 0 bf16, 1 fp16
+extern "C" int acth_act_dtype(void) { return ACTH_F16 ? 1 : 0; }

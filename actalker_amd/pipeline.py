@@ -143,6 +143,18 @@ def gate_masks(gate, face_mask: torch.Tensor, mouth_mask: torch.Tensor, exp_mask
 
 
 # ------------------------------------------------------------------------------------------ backend
+def _bits_equal(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Per leading index (frame), whether the two tensors' elements are bitwise equal (so -0.0 != +0.0, unlike
+    ``==``): the raw bits compared as integers of the element width."""
+    it = {2: torch.int16, 4: torch.int32, 8: torch.int64}[a.element_size()]
+    n = a.shape[0]
+    return (a.reshape(n, -1).view(it) == b.reshape(n, -1).view(it)).all(-1)
+
+
+def _same_bits(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return a.shape == b.shape and a.dtype == b.dtype and bool(_bits_equal(a.reshape(1, -1), b.reshape(1, -1)).all())
+
+
 class HipBackend:
     """Runs units through the HIP UNet (forward_tokens) and the fused guidance/Euler kernel.
     ``masks`` = (face_mask, mouth_mask, exp_mask), each (1, 1, H_px, W_px) (pipeline:636-646)."""
@@ -167,9 +179,11 @@ class HipBackend:
         # conditioning in device layouts, converted once per run
         self.img = ops.nchw_to_tokens(image_latents.to(dev).float(), out_dtype=torch.float32)     # (nb*T*S, 4)
         self.ide = image_embeddings.to(dev, cdt).reshape(nb, T, -1)                               # (nb, T, 1024)
-        self.aud = (audio_prompts.to(dev, torch.float32) * self.gate[0]).to(cdt)                  # (nb, T, 32, 1024)
+        # gated prompts (pipeline:724); "+ 0.0" turns the -0.0 of a negative prompt times gate 0 into +0.0, so branches
+        # whose gated prompts are equal are also bitwise equal (frame_equal / branch_twins compare bits)
+        self.aud = (audio_prompts.to(dev, torch.float32) * self.gate[0] + 0.0).to(cdt)            # (nb, T, 32, 1024)
         self.n_audio = self.aud.shape[2]
-        self.vas = (vasa_prompts.to(dev, torch.float32) * self.gate[1]).to(cdt).reshape(nb, T, -1)
+        self.vas = (vasa_prompts.to(dev, torch.float32) * self.gate[1] + 0.0).to(cdt).reshape(nb, T, -1)
         with ops.compute_dtype(cdt):
             self.pose = ops.nchw_to_tokens(pose_fea.to(dev))                                        # (P*S, 320)
         # pose features may hold P != T frames (the pipeline's pose list has N frames): the reference
@@ -198,7 +212,7 @@ class HipBackend:
             cls = list(range(nb))
             for c in range(1, nb):
                 for e in range(c):
-                    if cls[e] == e and torch.equal(img[c], img[e]) and torch.equal(self.added[c], self.added[e]):
+                    if cls[e] == e and _same_bits(img[c], img[e]) and _same_bits(self.added[c], self.added[e]):
                         cls[c] = e
                         break
             self._prefix_cls = cls
@@ -220,9 +234,9 @@ class HipBackend:
             for e in range(c):
                 if e in twins:
                     continue
-                if (torch.equal(self.ide[c], self.ide[e]) and torch.equal(img[c], img[e])
-                        and torch.equal(self.aud[c], self.aud[e]) and torch.equal(self.vas[c], self.vas[e])
-                        and torch.equal(self.added[c], self.added[e])):
+                if (_same_bits(self.ide[c], self.ide[e]) and _same_bits(img[c], img[e])
+                        and _same_bits(self.aud[c], self.aud[e]) and _same_bits(self.vas[c], self.vas[e])
+                        and _same_bits(self.added[c], self.added[e])):
                     twins[c] = e
                     break
         return twins
@@ -239,11 +253,10 @@ class HipBackend:
             eq = torch.zeros((nb, nb, T), dtype=torch.bool)
             for c in range(nb):
                 for e in range(c):
-                    if not torch.equal(self.added[c], self.added[e]):
+                    if not _same_bits(self.added[c], self.added[e]):
                         continue
-                    m = ((img[c] == img[e]).all(-1) & (self.ide[c] == self.ide[e]).reshape(T, -1).all(-1)
-                         & (self.aud[c] == self.aud[e]).reshape(T, -1).all(-1)
-                         & (self.vas[c] == self.vas[e]).reshape(T, -1).all(-1))
+                    m = (_bits_equal(img[c], img[e]) & _bits_equal(self.ide[c], self.ide[e])
+                         & _bits_equal(self.aud[c], self.aud[e]) & _bits_equal(self.vas[c], self.vas[e]))
                     eq[c, e] = m.cpu()
             self._frame_eq = eq
         return self._frame_eq

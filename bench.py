@@ -506,11 +506,18 @@ def main():
     # warmup (packs weights, builds mask tables, warms the allocator)
     with torch.no_grad():
         pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.warmup)
+    # ACTH_TRACE_MARK=1: a spin kernel on each side of the timed loop, so a rocprofv3 kernel trace can be cut to
+    # exactly the timed steps (tools/trace_gaps.py); off by default
+    mark = os.environ.get("ACTH_TRACE_MARK") == "1"
     barrier()
+    if mark:
+        torch.cuda._sleep(1000)
     t_start = time.perf_counter()
     plan = []
     with torch.no_grad():
         out = pl.denoise(backend, inp["latents"], cfg, rank, world, group, steps=args.steps, plan_log=plan)
+    if mark:
+        torch.cuda._sleep(1000)
     barrier()
     elapsed = time.perf_counter() - t_start
     if world > 1:

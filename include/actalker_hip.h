@@ -282,6 +282,9 @@ int acth_cfg_euler_accum(const float* noise, const long long* unit_off, const fl
                          int F, int S, hipStream_t stream);
 int acth_div_counter(const float* acc, const float* cnt, float* out, int T, int S, hipStream_t stream);
 int acth_version(void);
+/* activation dtype the library was built for: 0 = bf16 (libactalker_hip.so), 1 = fp16 (libactalker_hip_f16.so);
+ * the same C ABI is exported by both, so a host binding checks this once after loading */
+int acth_act_dtype(void);
 /* diagnostics: per-workgroup s_memtime phase stamps of the last phased-GEMM launch made with tile bit
  * 0x400 (entry, prologue landed, main loop done, epilogue done), n_wgs x 4 values copied to host */
 int acth_debug_gemm_stamps(unsigned long long* host_dst, int n_wgs);

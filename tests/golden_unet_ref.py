@@ -19,6 +19,9 @@ and mamba-ssm's selective_scan_ref are restatements.
 * ``full_half`` / ``full_mode0`` / ``full_mode2``: the real 1.775 B-parameter UNet (widths 320/640/1280/1280,
   heads 5/10/20/20) at 576x1024, B = 1 x F = 2, the inputs and weights of tests/golden_full.py's ``half`` /
   ``mode0`` / ``mode2`` cases, so the same fixtures also pin the oracle's full-geometry outputs.
+* ``win14_mode0``: the same UNet at the headline window shape, 576x1024, B = 3 CFG branches x F = 14 frames, mode 0
+  (tests/golden_win14.py: the inputs stacked as the reference pipeline stacks one window's uncond / drop audio+vasa /
+  drop vasa branches).
 * ``c1_face0``: the same UNet at BASELINE C1's geometry, 576x576 (latent 72x72; levels 72x72 / 36x36 / 18x18 /
   9x9), B = 1 x F = 2, mode 0 (gate [1, 0], zero VASA tokens) with a centre face box as the audio mask.
 
@@ -38,7 +41,7 @@ TINY_CASES = ("tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box",
 # the reference's shipped window: config/inference.yaml:4 n_sample_frames = 25 -> Inference.py:573 frames_per_batch,
 # so every temporal block (attention.py:431-433, the temporal ResBlocks' (3,1,1) convs and GroupNorm) spans 25 frames
 F25 = 25
-FULL_CASES = ("full_half", "full_mode0", "full_mode2", "c1_face0")
+FULL_CASES = ("full_half", "full_mode0", "full_mode2", "c1_face0", "win14_mode0")
 CASES = TINY_CASES + FULL_CASES
 SIGMA = 1.6555  # Karras step 12 of 25; t = 0.25 ln sigma
 
@@ -86,6 +89,9 @@ def case_inputs(case: str):
         return gf.case_inputs(case.split("_", 1)[1])
     if case == "c1_face0":
         return gf.case_inputs("face0", h_px=576, w_px=576)
+    if case == "win14_mode0":
+        from tests import golden_win14 as gw
+        return gw.reference_inputs()
     raise ValueError(case)
 
 

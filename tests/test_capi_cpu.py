@@ -37,6 +37,12 @@ def test_library_exports_every_declared_symbol(which):
 
 
 @pytest.mark.parametrize("which", LIB_DTYPES)
+def test_library_reports_its_activation_dtype(which):
+    """Both builds export the same ABI; load() checks acth_act_dtype() so a bf16 build is never used for fp16."""
+    assert load(which).acth_act_dtype() == (1 if which == "fp16" else 0)
+
+
+@pytest.mark.parametrize("which", LIB_DTYPES)
 def test_struct_layouts_match_header(which):
     lib = load(which)
     assert lib.acth_gemm_desc_size() == ctypes.sizeof(_lib.GemmDesc)

@@ -376,6 +376,50 @@ def test_pipeline_loop_twin_branches(dev, tiny, gate, twins):
     assert err < 5e-2, err
 
 
+def test_pipeline_loop_padding_window_twins(dev, tiny):
+    """Mode 2 with the pipeline's padding (pipeline:170-184): past frame N every branch's audio / VASA prompt is the
+    uncond pad (the first uncond frame repeated), and branches 1-3 share the ID embedding and image latents, so in a
+    window made only of padding frames branches 2 and 3 receive branch 1's inputs. The loop evaluates 10 instead of
+    12 (window, branch) units on the steps with such a window (shift 0 at N = 4, fpb 2: window [4, 5]) and matches
+    the loop that evaluates all four branches everywhere on the real HIP UNet."""
+    from actalker_amd import pipeline as pl
+    unet, sd, cfg = tiny
+    N, fpb, H, W = 4, 2, 16, 32
+    T = N + fpb
+    g = torch.Generator().manual_seed(29)
+    latents = 0.18215 * torch.randn(1, 1, 4, H, W, generator=g) + 700.0 * torch.randn(1, T, 4, H, W, generator=g)
+    il = torch.randn(1, T, 4, H, W, generator=g)
+    imgl = torch.cat([torch.zeros_like(il), il, il, il])
+    e = torch.randn(1, T, 1, 1024, generator=g)
+    ide = torch.cat([torch.zeros_like(e), e, e, e])
+    a_u, a_c = torch.randn(1, T, 32, 1024, generator=g), torch.randn(1, T, 32, 1024, generator=g)
+    v_u, v_c = torch.randn(1, T, 1, 1024, generator=g), torch.randn(1, T, 1, 1024, generator=g)
+    a_u[:, N:] = a_u[:, :1]              # pad_uncond_audio = uncond_audio[:1] repeated (pipeline:175-179)
+    a_c[:, N:] = a_u[:, :1]
+    v_u[:, N:] = v_u[:, :1]
+    v_c[:, N:] = v_u[:, :1]
+    aud = torch.cat([a_u, a_u, a_c, a_c])
+    vas = torch.cat([v_u, v_u, v_u, v_c])
+    pose = 0.1 * torch.randn(1, T, 64, H, W, generator=g)
+    added = torch.tensor([[12.5, 12.0, 20.0]] * 4)
+    lower = torch.zeros(1, 1, 8 * H, 8 * W)
+    lower[..., 4 * H:, :] = 1.0
+    masks = (torch.ones(1, 1, 8 * H, 8 * W), lower, 1 - lower)
+    backend = pl.HipBackend(unet, H, W, masks, [1, 1], added, T, fpb, imgl, ide, aud, vas, pose)
+    assert backend.branch_twins() == {}
+    lc = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, num_inference_steps=25)
+    plan = []
+    with torch.no_grad():
+        got = pl.denoise(backend, latents, lc, steps=3, plan_log=plan)
+        lc4 = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, overlap=0, shift_offset=1, num_inference_steps=25,
+                            dedup_branches=False)
+        plan4 = []
+        all4 = pl.denoise(backend, latents, lc4, steps=3, plan_log=plan4)
+    assert [p["units"] for p in plan] == [10, 12, 10], plan
+    assert [p["units"] for p in plan4] == [12, 12, 12], plan4
+    assert rel(got, all4) < 1e-2
+
+
 def _oracle_loop(unet_fn, latents, imgl, ide, aud, vas, pose, added, masks, gate, N, fpb, steps):
     """oracle.denoise_loop truncated to `steps` sampler steps (same schedule)."""
     sig, ts = ref.euler_karras_tables(25)

@@ -34,6 +34,10 @@ def main(iters=3, only_quad=False):
         variants = [("pair", 1, xdbl), ("pairbf", 1, xbf), ("quad", 1, xbf)]
         if only_quad:
             variants = [("quad", 1, xbf)]
+        if "--seg" in sys.argv:
+            # the two-pass wavefront-segmented form (scan_kernel<R, PASS>: each chunk from a zero state, the
+            # chunk-end states carried across in pass 2; fp32 xdbl rows) beside the single-pass paired-lane kernel
+            variants = [("pairbf", 1, xbf), ("seg2", 2, xdbl), ("seg4", 4, xdbl), ("seg8", 8, xdbl)]
         for name, nc, xd in variants:
             ops.SCAN_ALGO = 1 if name == "quad" else 0
             args = dict(nb=nb, L=L, R=R, n_keep=n_keep, nchunks=nc)
@@ -70,3 +74,5 @@ def main(iters=3, only_quad=False):
 
 if __name__ == "__main__":
     main(only_quad="--quad" in sys.argv)
+# C5's per-rank load (8 GPUs, mode 2: 5 units x 14 frames = 70 batch elements per UNet call):
+#   python tools/bench_scan.py --seg --shape 70,9249,640,20 70,2337,1280,40 70,609,2560,80

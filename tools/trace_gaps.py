@@ -19,6 +19,9 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--stats-csv", default=None,
+                    help="also write per-kernel stats of the timed steps (Name, Calls, TotalDurationNs, AverageNs, "
+                         "Percentage, MsPerStep) to this file")
     a = ap.parse_args()
     rows = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
                    for r in csv.DictReader(open(a.csv))), key=lambda x: x[0])
@@ -47,6 +50,17 @@ def main():
         if g >= 5e3:
             pair[(p, n)][0] += 1
             pair[(p, n)][1] += g
+    if a.stats_csv:
+        agg = collections.defaultdict(lambda: [0, 0])
+        for s, e, n in ks:
+            agg[n][0] += 1
+            agg[n][1] += e - s
+        tot = sum(v[1] for v in agg.values())
+        with open(a.stats_csv, "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MsPerStep"])
+            for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+                w.writerow([n, c, t, round(t / c, 1), round(100.0 * t / tot, 3), round(t / 1e6 / a.steps, 3)])
     print("largest idle sources (gaps >= 5 us, grouped by kernel pair):")
     for (p, n), (c, g) in sorted(pair.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"  {g / 1e6:7.3f} ms {c:5d}x  {p}  ->  {n}")

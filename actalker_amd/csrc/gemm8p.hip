@@ -567,8 +567,8 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     // loop is branch-free, and each lane keeps one 8-column chunk across the quadrant's rows (its bias
     // chunk in registers, row-strided pointers) instead of re-deriving 64-bit addresses per chunk.
     // Measured with tools/gemm_stamps.py: the generic loop spent ~29k cycles per 256x320 tile.
-    const bool fast = p.act == 0 && !p.out_f32 && p.orow_div >= p.M && vec_ok && (p.N & 7) == 0 && !p.rmap &&
-                      (!p.rowbias || rb_lds);
+    const bool fast = p.act == 0 && !p.out_f32 && (p.orow_div >= p.M || p.orow_div % SR == 0) && vec_ok &&
+                      (p.N & 7) == 0 && !p.rmap && (!p.rowbias || rb_lds);
     auto fast_epilogue = [&](auto res_c, auto mix_c, auto rb_c) {
       constexpr bool RES = decltype(res_c)::value, MIXB = decltype(mix_c)::value, RB = decltype(rb_c)::value;
       constexpr int RPI = 64 / CPR, LPI = RPI * CPR, NIT = (SR + RPI - 1) / RPI;
@@ -606,7 +606,9 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
         const int col = q_col(qn), rowf = q_row(qm);
         const float4 b0 = *reinterpret_cast<const float4*>(&sbias[lc0 + c8]);
         const float4 b1 = *reinterpret_cast<const float4*>(&sbias[lc0 + c8 + 4]);
-        bf16_t* cp = (bf16_t*)p.C + (size_t)(rowf + p.orow_off) * p.ldc + col;
+        // output rows through the remap (in_proj's xz rows into the scan sequence): a wave's SR rows lie in one
+        // remap group (fast requires orow_div % SR == 0), so one division per quadrant
+        bf16_t* cp = (bf16_t*)p.C + (out_row(p, rowf - r0) + r0) * p.ldc + col;
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
           const int r = r0 + it * RPI;
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       const int r0 = lane / CPR, c8 = (lane - r0 * CPR) * 8;
       auto from_slab = [&](int qm, int qn) {
         const int rowf = tile_m + qm * 128 + wr * SR + r0, col = tile_n + qn * (BN_ / 2) + wc * SC + c8;
-        bf16_t* cp = (bf16_t*)p.C + (size_t)(rowf + p.orow_off) * p.ldc + col;
+        bf16_t* cp = (bf16_t*)p.C + (out_row(p, rowf - r0) + r0) * p.ldc + col;
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
           const int r = r0 + it * RPI;

@@ -381,6 +381,33 @@ def test_conv3x3(dev, B, H, W, C1, C2, Cout, mode):
     assert rel(out, refo.permute(0, 2, 3, 1).reshape(-1, Cout)) < 1e-2
 
 
+@pytest.mark.parametrize("tile,N", [(5, 320), (4, 256), (5, 640)])
+@pytest.mark.parametrize("OD", [576, 144])
+def test_gemm_orow_remap_fast_epilogue(dev, tile, N, OD):
+    """Output-row remap (row m -> (m / OD) * OS + m % OD: the Mamba in_proj writing S-token images into
+    L-row scan sequences) through the phased kernels' fast epilogue -- taken when every wave's rows lie in one
+    remap group (OD % 32 == 0 at 256x320, % 64 at 256x256: 576) -- and the generic one (OD = 144), with bias
+    and residual; the slots between groups stay untouched."""
+    g = torch.Generator().manual_seed(OD + N)
+    K, OS = 320, OD + 33
+    M = 5 * OD + OD // 2
+    a = bf(rnd(M, K, g=g))
+    w = bf(rnd(N, K, scale=K ** -0.5, g=g))
+    b = rnd(N, g=g)
+    r = bf(rnd(M, N, g=g))
+    ngrp = -(-M // OD)
+    out = torch.zeros(ngrp * OS, N, device=dev, dtype=ops.act_dtype())
+    ops.gemm(a.to(dev), w.to(dev), bias=b.to(dev), residual=r.to(dev), out=out, orow=(OD, OS, 0), tile=tile)
+    src = torch.arange(M)
+    dst = (src // OD) * OS + src % OD
+    want = a.float() @ w.float().t() + b + r.float()
+    got = out.cpu()
+    assert rel(got[dst], want) < 1e-2
+    keep = torch.ones(ngrp * OS, dtype=torch.bool)
+    keep[dst] = False
+    assert got[keep].abs().max().item() == 0.0
+
+
 def test_gemm_over_2gib(dev):
     """A operands past the 2 GiB buffer extent run as row chunks (acth_gemm's descriptor rebasing):
     a strided dense A inside 4.5 GB rows (the mode-2 x_proj read of Mamba xz) with row-bias images and

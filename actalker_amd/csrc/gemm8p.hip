@@ -25,7 +25,10 @@ using namespace gemm;
 
 // 1: 3x3-conv K order with the 64-channel slice outer and the tap inner (L2 reuse of the nine taps'
 // shared window). Measured slower in isolation (level-0 conv 951 -> 881 TFLOP/s, level 2 1106 -> 945,
-// profiles/r3_step31_conv_order_rejected.log), so off
+// profiles/r3_step31_conv_order_rejected.log), so off. 2: (ky, slice, kx), the three kx taps of a slice in
+// consecutive K tiles: 11-20 % slower on every conv shape (level 0 985 -> 875, level 1 1066 -> 910, level 2
+// 1133 -> 940; profiles/r5_conv_korder_rejected.log) -- re-deriving the four rows' tap offsets every K tile
+// costs more than the L2 reuse returns
 #ifndef G8_CONV_CMAJOR
 #define G8_CONV_CMAJOR 0
 #endif
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int kfull = p.K / 64;
 
   // per-K-tile staging parameters, advanced by prep_k() in K order
-  int s_tap = 0, s_c0 = 0;
+  int s_tap = 0, s_c0 = 0, s_ky = 0, s_kx = 0;
   int k_c0 = 0, k_k0 = 0, k_kb = 0;
   bool k_second = false, k_tail = false;
   const int ntap = AMODE == 0 ? 1 : p.K / cin;
@@ -241,7 +244,19 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     k_kb = k_k0;
     if (AMODE == 0) {
       k_c0 = k_k0;
-    } else if (AMODE == 1 && G8_CONV_CMAJOR) {
+    } else if (AMODE == 1 && G8_CONV_CMAJOR == 2) {
+      // (ky, 64-channel slice, kx): the three kx taps of a slice -- the same image pixels shifted by one --
+      // are consecutive K tiles, so their re-reads meet in L2 one K tile apart instead of a channel pass apart
+      const int tap = s_ky * 3 + s_kx;
+      set_tap(tap);
+      k_c0 = s_c0;
+      k_kb = tap * cin + s_c0;
+      if (++s_kx == 3) {
+        s_kx = 0;
+        s_c0 += 64;
+        if (s_c0 == cin) { s_c0 = 0; ++s_ky; }
+      }
+    } else if (AMODE == 1 && G8_CONV_CMAJOR == 1) {
       // 3x3 conv, 64-channel slice outer and tap inner: the nine taps of one slice read one ~4-image-row
       // window of it in consecutive K tiles, so the window stays in L2 (tap-major order re-reads every
       // input row from HBM once per tap row: 4.3 GB per level-0 conv dispatch for ~1.5 GB of operands).

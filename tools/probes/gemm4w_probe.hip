@@ -85,6 +85,29 @@ __global__ __launch_bounds__(256, 1) void gemm4w(const uint16_t* A, const uint16
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#if PF_KSTEP == 2
+  // hand-interleaved body: the next K tile's 16 LDS-DMA pieces and k-step 1's 16 fragment reads are spread
+  // one each between groups of 4 of k-step 0's 64 MFMAs (sched_group_barrier), k-step 1's MFMAs follow
+  auto body = [&](int cur, bool more, int kt) {
+    rd(cur, 0, 0);
+    if (more) stage(kt + 1, cur ^ 1);
+    rd(cur, 1, 1);
+    mma(0);
+    mma(1);
+    // ordering hints for the region: 8 ds_read, then repeat {4 MFMA, 1 DS read, 1 VMEM} x 16
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // k-step 0 fragments first
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read (k-step 1)
+      if (more) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM (DMA)
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);   // k-step 1 MFMAs
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  for (int kt = 0; kt + 1 < nk; ++kt) body(kt & 1, true, kt);
+  body((nk - 1) & 1, false, nk - 1);
+#else
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
@@ -101,6 +124,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w(const uint16_t* A, const uint16
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+#endif
   if (!STORE) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)

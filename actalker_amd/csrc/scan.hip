@@ -28,9 +28,6 @@
 
 #define SC_T 16
 #define SC_THREADS 128
-#ifndef SCAN_YDEFER
-#define SCAN_YDEFER 1
-#endif
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -282,12 +279,6 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
   __shared__ __attribute__((aligned(16))) bf16_t us[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) bf16_t ys[SC_T * SP_CH];
   __shared__ __attribute__((aligned(16))) float dls[SC_T * DLP];
-#if SCAN_YDEFER
-  // full tiles: each lane's half-sum of C . h per token, parked here; the pair sum, D u and the bf16
-  // conversion run once per output in the tile's store phase instead of per lane and token in the serial loop
-  __shared__ __attribute__((aligned(16))) float yps[SC_T * NT];
-  __shared__ __attribute__((aligned(16))) float dsks[SP_CH];
-#endif
 
   const int k = kyi, b = bzi - (second ? nb0 : 0);
   const int t = threadIdx.x;
@@ -333,9 +324,6 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
     h[n / 2][n % 2] = 0.0f;
   }
   const float dsk = p.Dskip ? p.Dskip[k * p.D + dd] : 0.0f;
-#if SCAN_YDEFER
-  if (half == 0) dsks[cl] = dsk;      // read after the first tile's barriers
-#endif
 
   const bf16_t* ub = (const bf16_t*)p.u + (size_t)b * p.L * p.ldu + (size_t)k * p.u_gstride + dbase;
   const float* xb = p.xdbl + (size_t)b * p.L * p.ldx + k * W;
@@ -560,13 +548,9 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
           h[n] = __builtin_elementwise_fma(ee[tt & 1][n], h[n], db[tt & 1][n]);
           y2 = __builtin_elementwise_fma(h[n], cc[n], y2);
         }
-#if SCAN_YDEFER
-        yps[tt * NT + t] = y2.x + y2.y;
-#else
         float y = y2.x + y2.y;
         y += pair_swap(y);
         ys[tt * SP_CH + cl] = f2bf(fmaf(dsk, uus[tt & 1], y));
-#endif
       }
     } else {
       for (int tt = 0; tt < nt; ++tt) token(tt);
@@ -576,37 +560,17 @@ __global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(cons
     {
       const int tt = t / U16, cc = (t % U16) * 8;
       const int i = i0 + tt;
-      uint4 v;
-#if SCAN_YDEFER
-      if (nt == SC_T) {
-        // y = (lane 2c's half-sum + lane 2c+1's) + D u: the serial loop's association (fma of D u last)
-        const float4* pp = reinterpret_cast<const float4*>(&yps[tt * NT + 2 * cc]);
-        const float4 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3];
-        const float4 d0 = *reinterpret_cast<const float4*>(&dsks[cc]);
-        const float4 d1 = *reinterpret_cast<const float4*>(&dsks[cc + 4]);
-        float uf[8];
-        unpack8(*reinterpret_cast<const uint4*>(&us[tt * SP_CH + cc]), uf);
-        const float ps[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,
-                              p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
-        const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-        float yv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) yv[e] = fmaf(dv[e], uf[e], ps[2 * e] + ps[2 * e + 1]);
-        v = pack8(yv);
-      } else {
-        v = *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
-      }
-#else
-      v = *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
-#endif
       if constexpr (XB) {
         const int l = pos_of(i);
         const bool ok = tt < nt && dbase + cc < p.D && l < p.n_keep;
+        const uint4 v = *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
         __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){v.x, v.y, v.z, v.w}, ry,
                                                (int)(ok ? (unsigned)(l * p.ldy + cc) * 2u : OOB), 0, 0);
       } else if (tt < nt && dbase + cc < p.D) {
         const int l = pos_of(i);
-        if (l < p.n_keep) *reinterpret_cast<uint4*>(yb + (size_t)l * p.ldy + cc) = v;
+        if (l < p.n_keep)
+          *reinterpret_cast<uint4*>(yb + (size_t)l * p.ldy + cc) =
+              *reinterpret_cast<const uint4*>(&ys[tt * SP_CH + cc]);
       }
     }
   };

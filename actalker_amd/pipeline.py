@@ -343,6 +343,21 @@ def broadcast_from_rank0(t: torch.Tensor, group=None) -> torch.Tensor:
     return t
 
 
+def all_gather_rows(dst: torch.Tensor, src: torch.Tensor, group=None):
+    """``dst`` = every rank's ``src`` rows, rank-major (all_gather_into_tensor). RCCL ("nccl") gathers device
+    tensors in place; another backend (gloo: the CPU tests, and ranks sharing one device) gathers host copies."""
+    import torch.distributed as dist
+    on_gpu = dist.get_backend(group) == "nccl"
+    if src.is_cuda == on_gpu:
+        dist.all_gather_into_tensor(dst, src, group=group)
+        return dst
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    tmp = torch.empty(dst.shape, dtype=dst.dtype, device=dev)
+    dist.all_gather_into_tensor(tmp, src.to(dev), group=group)
+    dst.copy_(tmp)
+    return dst
+
+
 @dataclass
 class LoopConfig:
     num_frames: int
@@ -453,9 +468,8 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
                 chunk = my_units[c0:c1]
                 backend.run_units(lat, chunk, frames, timesteps[i], sigmas[i], local, c0 * rows_per_unit)
         if world > 1:
-            import torch.distributed as dist
             n = cap * rows_per_unit
-            dist.all_gather_into_tensor(gathered[:world * n], local[:n], group=group)
+            all_gather_rows(gathered[:world * n], local[:n], group)
         unit_rows = [[owner_row[index[(w, tw[w].get(c, c))]] for c in range(4)] for w in range(n_windows)]
         g = cfg.guidance if cfg.guidance_schedule is None else cfg.guidance_schedule[i]
         lat = backend.step_windows(lat, gathered, unit_rows, frames, g, sigmas[i], sigmas[i + 1])

@@ -115,16 +115,27 @@ def gemm_algorithmic_bytes(a, w, M, N, K, kw):
     return a_elems * esz + N * K * esz + M * n_out * out_b + extra
 
 
+PMC_WORKLOAD = None     # this run's workload key (set in main); PMC bytes are reported for that workload only
+
+
+def workload_key(mode, height, width, frames, fpb, dtype):
+    return f"mode{mode} {height}x{width} f{frames} fpb{fpb} {dtype}"
+
+
 def pmc_traffic(family="acth_gemm"):
     """Per-kernel-family HBM bytes measured by rocprofv3 PMC passes of this command over one sampler
     step (tools/pmc_pass.sh -> tools/pmc_summary.py --json -> profiles/pmc_traffic.json), or None:
-    {hbm_bytes_per_launch (per kernel dispatch), dispatches, read_bytes, write_bytes, source}."""
+    {hbm_bytes_per_launch (per kernel dispatch), dispatches, read_bytes, write_bytes, source}. None as well
+    when the counted run's workload (the file's "_workload") is not this run's."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            return json.load(fh).get(family)
+            d = json.load(fh)
     except (OSError, ValueError):
         return None
+    if d.get("_workload") is None or d.get("_workload") != PMC_WORKLOAD:
+        return None
+    return d.get(family)
 
 
 class GemmTimer:
@@ -463,6 +474,8 @@ def main():
     N = args.frames_per_gpu * world
     fpb = args.fpb
     H, W = args.height, args.width
+    global PMC_WORKLOAD
+    PMC_WORKLOAD = workload_key(args.mode, H, W, args.frames_per_gpu, fpb, args.dtype)
     t0 = time.time()
     unet_cpu = build_unet(dev)
     unet = unet_cpu.to(dev)

@@ -168,7 +168,9 @@ def _worker(rank, world, port, N, fpb, steps, q, twin=False, pad=False, shift=1)
             backend = (TwinCpuBackend if twin else CpuBackend)(imgl, latents.shape[3], latents.shape[4], N + fpb, fpb)
         cfg = pl.LoopConfig(num_frames=N, frames_per_batch=fpb, shift_offset=shift, units_per_call=2)
         out = pl.denoise(backend, latents, cfg, rank, world, steps=steps)
-        q.put((rank, out))
+        # by value (numpy): a tensor put on the queue travels through shared memory whose descriptor
+        # the parent fetches from this process, which may have exited by then
+        q.put((rank, out.detach().cpu().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -218,7 +220,7 @@ def test_sharded_loop_matches_single_process(world, N, fpb):
     procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=300) for _ in range(world))
+    outs = {r: torch.from_numpy(a) for r, a in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -275,7 +277,7 @@ def test_twin_branch_evaluated_once_matches_four_branch_loop(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, N, fpb, steps, q, True)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=300) for _ in range(world))
+    outs = {r: torch.from_numpy(a) for r, a in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -339,7 +341,7 @@ def test_padding_window_twins_match_four_branch_loop(world, N, fpb):
              for r in range(world)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=300) for _ in range(world))
+    outs = {r: torch.from_numpy(a) for r, a in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -446,7 +448,9 @@ def _svd_worker(rank, world, port, q):
         out = pipe(ref, torch.zeros(1, 512), pose, masks, masks, a, a, v, v, height=H, width=W, num_frames=N,
                    num_inference_steps=3, frames_per_batch=fpb, overlap=0, shift_offset=1, output_type="latent",
                    generator=None, world=world, rank=rank).frames
-        q.put((rank, out))
+        # by value (numpy): a tensor put on the queue travels through shared memory whose descriptor
+        # the parent fetches from this process, which may have exited by then
+        q.put((rank, out.detach().cpu().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -459,7 +463,7 @@ def test_svd_pipeline_ranks_agree_without_generator():
     procs = [ctx.Process(target=_svd_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=300) for _ in range(world))
+    outs = {r: torch.from_numpy(a) for r, a in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -43,7 +43,8 @@ def main():
                 "selective_scan": lambda k: "scan" in k, "groupnorm": lambda k: k.startswith("gn_"),
                 "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k,
                 "mamba_combine": lambda k: "mamba_combine" in k}
-        res = {}
+        # the bench configuration the counted run used (bench.py only reports traffic for that same workload)
+        res = {"_workload": sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None}
         for fam, match in fams.items():
             g = [r for r in rows if match(r[0].split("(")[0].replace("void ", ""))]
             n = sum(r[1] for r in g)

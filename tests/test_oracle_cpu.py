@@ -156,6 +156,24 @@ def test_oracle_unet_matches_reference_run(case):
     assert rel < 1e-4, rel
 
 
+def test_oracle_unet_twin_inputs_give_bitwise_equal_outputs():
+    """The C1 fixture generator (tools/gen_golden_c1.py) evaluates a CFG branch whose inputs are bitwise an earlier
+    branch's once and reuses that output, as batch-1 oracle calls. That shortcut is exact iff a batch-1 oracle call is
+    a deterministic function of its inputs: two calls on bitwise-equal inputs (separate tensors) must agree bitwise."""
+    from tests import golden_unet_ref as gu
+    unet = gu.build_hip_unet("tiny_mode0")
+    sd = {k: v.detach().float() for k, v in unet.state_dict().items()}
+    sample, t, ehs, added, pose, masks = gu.case_inputs("tiny_mode0")
+    F = sample.shape[1]
+    outs = []
+    with torch.no_grad():
+        for _ in range(2):
+            e = (ehs[0][:F].clone(), [x[:F].clone() for x in ehs[1]])
+            outs.append(ref.unet_forward(sd, sample[:1].clone(), t, e, added[:1].clone(), pose[:1].clone(),
+                                         {"ip_adapter_masks": [m.clone() for m in masks]}, cfg=gu.oracle_cfg("tiny_mode0")))
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("case", ["half", "mode0", "mode2"])
 def test_oracle_full_geometry_fixture_matches_reference_run(case):
     """The full-geometry oracle fixtures (576x1024, real widths; tools/gen_golden_full.py) against the reference

@@ -118,8 +118,8 @@ def gemm_algorithmic_bytes(a, w, M, N, K, kw):
 PMC_WORKLOAD = None     # this run's workload key (set in main); PMC bytes are reported for that workload only
 
 
-def workload_key(mode, height, width, frames, fpb, dtype):
-    return f"mode{mode} {height}x{width} f{frames} fpb{fpb} {dtype}"
+def workload_key(mode, height, width, frames, fpb, dtype, world=1):
+    return f"mode{mode} {height}x{width} f{frames} fpb{fpb} {dtype}" + (f" world{world}" if world > 1 else "")
 
 
 def pmc_traffic(family="acth_gemm"):
@@ -461,12 +461,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one rank per GPU; ACTH_DIST_BACKEND=gloo (with ranks sharing a device: LOCAL_RANK modulo the visible GPUs)
+    # rehearses the multi-rank bench on a one-GPU box -- RCCL refuses two ranks on one device
+    # (profiles/r5_rccl_same_gpu_probe.log) -- and its timings then mean nothing
+    backend_name = os.environ.get("ACTH_DIST_BACKEND", "nccl")
+    dev_idx = local_rank % max(1, torch.cuda.device_count()) if backend_name != "nccl" else local_rank
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     group = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend_name == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend_name)
 
     from actalker_amd import pipeline as pl
 
@@ -475,7 +483,7 @@ def main():
     fpb = args.fpb
     H, W = args.height, args.width
     global PMC_WORKLOAD
-    PMC_WORKLOAD = workload_key(args.mode, H, W, args.frames_per_gpu, fpb, args.dtype)
+    PMC_WORKLOAD = workload_key(args.mode, H, W, args.frames_per_gpu, fpb, args.dtype, world)
     t0 = time.time()
     unet_cpu = build_unet(dev)
     unet = unet_cpu.to(dev)

@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(const ActhConvDirectDe
 }  // namespace
 
 extern "C" int acth_conv_direct(const ActhConvDirectDesc* d, hipStream_t stream) {
+  if (d && d->B == 0) return ACTH_OK;   // empty batch: nothing read or written
   if (!d || !d->x || !d->w || !d->y) return ACTH_EINVAL;
   if (d->Cin <= 0 || d->Cout <= 0 || d->ldx < d->Cin || d->ldy < d->Cout) return ACTH_EINVAL;
   if (d->act != 0 && d->act != 1 && d->act != 3) return ACTH_EINVAL;

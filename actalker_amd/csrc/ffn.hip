@@ -415,6 +415,7 @@ __global__ __launch_bounds__(512, 1) void ffn_geglu_kernel(const ActhFfnDesc p, 
 }
 
 extern "C" int acth_geglu_ffn(const ActhFfnDesc* d, hipStream_t stream) {
+  if (d && d->M == 0) return ACTH_OK;   // no rows: nothing read or written
   if (!d || !d->x || !d->w1 || !d->w2 || !d->y) return ACTH_EINVAL;
   if (d->C != 320 || d->M < 0) return ACTH_EINVAL;
   if (d->M == 0) return ACTH_OK;

@@ -268,6 +268,7 @@ static int gemm_split_rows(const ActhGemmDesc* d, hipStream_t stream) {
 }
 
 extern "C" int acth_gemm(const ActhGemmDesc* d, hipStream_t stream) {
+  if (d && d->M == 0) return ACTH_OK;   // no rows: nothing read or written
   if (!d || !d->A || !d->B || !d->C) return ACTH_EINVAL;
   // rows < 2^22: the epilogues divide row indices with a float-reciprocal estimate (udiv22)
   if (d->M < 0 || d->M >= (1 << 22) || d->N <= 0 || d->K <= 0) return ACTH_EINVAL;

@@ -210,6 +210,7 @@ __global__ __launch_bounds__(256) void layernorm_scalar_kernel(const ActhLayerNo
 }
 
 extern "C" int acth_layernorm(const ActhLayerNormDesc* d, hipStream_t stream) {
+  if (d && d->M == 0) return ACTH_OK;   // no rows: nothing read or written
   if (d && d->x && d->y && d->C > 0 && (d->C % 8 || d->ldx % 8 || d->ldy % 8) && !d->add && !d->sum_out &&
       d->ldx >= d->C && d->ldy >= d->C) {
     if (d->M == 0) return ACTH_OK;
@@ -410,6 +411,7 @@ extern "C" size_t acth_groupnorm_workspace_size(int M, int C, int G, int rows_pe
 }
 
 extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
+  if (d && d->M == 0) return ACTH_OK;   // no rows: nothing read or written
   if (!d || !d->x || !d->y || !d->ws || !d->gamma || !d->beta) return ACTH_EINVAL;
   if (d->C % 8 || d->C1 % 8 || d->G <= 0 || d->C % d->G || d->rows_per_stat <= 0) return ACTH_EINVAL;
   if (d->M % d->rows_per_stat) return ACTH_EINVAL;
@@ -554,6 +556,7 @@ __global__ __launch_bounds__(256) void mamba_combine_kernel(const ActhMambaCombi
 }
 
 extern "C" int acth_mamba_combine_ln(const ActhMambaCombineDesc* d, hipStream_t stream) {
+  if (d && d->M == 0) return ACTH_OK;   // no rows: nothing read or written
   if (!d || !d->y || !d->gamma || !d->beta) return ACTH_EINVAL;
   if (d->C % 8 || d->C > 64 * 8 * 6 || d->S <= 0 || d->M % d->S) return ACTH_EINVAL;
   if (((size_t)d->gamma | (size_t)d->beta) & 15) return ACTH_EINVAL;

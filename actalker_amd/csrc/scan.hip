@@ -892,6 +892,7 @@ extern "C" size_t acth_selective_scan_workspace_size(int nb, int G, int D, int n
 
 // argument checks and derived fields (nchunks / chunk_len); 1 = valid with nothing to do (n_keep 0)
 static int scan_prepare(ActhScanDesc& d) {
+  if (d.nb == 0) return 1;                                          // empty batch: nothing read or written
   if (!d.u || !d.xdbl || !d.A_log || !d.y0) return ACTH_EINVAL;
   if (d.R > 0 && (!d.dt_w || d.delta)) return ACTH_EINVAL;          // exactly one delta source
   if (d.R == 0 && !d.delta) return ACTH_EINVAL;

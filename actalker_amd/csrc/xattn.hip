@@ -549,6 +549,7 @@ extern "C" int acth_debug_xattn_stamps(unsigned long long* host_dst, int n_wgs, 
 }
 
 extern "C" int acth_xattn(const ActhXattnDesc* d, hipStream_t stream) {
+  if (d && d->M == 0) return ACTH_OK;   // no rows: nothing read or written
   if (!d || !d->h || !d->base || !d->out) return ACTH_EINVAL;
   if (d->C != XA_C || d->H * 64 != d->C || d->M <= 0) return ACTH_EINVAL;
   if (d->rows_per_ctx <= 0 || d->rows_per_ctx % XA_TOK || d->M % d->rows_per_ctx || d->S <= 0) return ACTH_EINVAL;

@@ -18,7 +18,10 @@
  *     below is IEEE half; fp32 operands and all descriptors are unchanged;
  *   - stream-ordered on `stream`; no allocation, no host synchronisation (graph-capturable);
  *   - return ACTH_OK (0), ACTH_EINVAL (-1) for a rejected shape/alignment, or ACTH_ELAUNCH (-2)
- *     when the launch failed.
+ *     when the launch failed;
+ *   - a call with no work (zero rows / an empty batch: M, B, nbatch, nb, Sq = 0, as torch ops accept empty
+ *     tensors) returns ACTH_OK without launching and reads no pointer (an empty tensor's data pointer may
+ *     be NULL); negative sizes stay ACTH_EINVAL.
  */
 #ifndef ACTALKER_HIP_H
 #define ACTALKER_HIP_H

@@ -62,6 +62,7 @@ def test_struct_layouts_match_header(which):
 def test_invalid_arguments_rejected_without_launch(which):
     lib = load(which)
     d = _lib.GemmDesc()
+    d.M, d.N, d.K = 8, 8, 16
     assert lib.acth_gemm(ctypes.byref(d), None) == -1               # null operands
     d.A, d.B, d.C = 16, 16, 16
     d.M, d.N, d.K, d.lda, d.ldb, d.ldc = 8, 8, 12, 16, 16, 8           # K % 8 != 0
@@ -80,6 +81,36 @@ def test_invalid_arguments_rejected_without_launch(which):
     c.stride, c.Ho = 2, 8                                                   # Ho != (H-1)//2 + 1
     assert lib.acth_conv_direct(ctypes.byref(c), None) == -1
     assert lib.acth_softmax_rows(16, 4, 16, 8, 2, 8, 1.0, None) == -1        # ldx < cols
+
+
+@pytest.mark.parametrize("which", LIB_DTYPES)
+def test_zero_work_calls_are_noops(which):
+    """A call with no rows / an empty batch returns ACTH_OK without reading its (here NULL) pointers, as the torch
+    ops it replaces accept empty tensors; a negative size is still rejected."""
+    lib = load(which)
+    cases = [
+        (lib.acth_gemm, _lib.GemmDesc, dict(N=8, K=16), "M"),
+        (lib.acth_flash_attn, _lib.AttnDesc, dict(nheads=1, Sq=64, Skv=64), "nbatch"),
+        (lib.acth_temporal_attn, _lib.TemporalAttnDesc, dict(F=14, S=4, H=1), "B"),
+        (lib.acth_ip_attn, _lib.IpAttnDesc, dict(H=5, rows_per_ctx=64, S=64), "M"),
+        (lib.acth_xattn, _lib.XattnDesc, dict(C=320, H=5, rows_per_ctx=64, S=64), "M"),
+        (lib.acth_geglu_ffn, _lib.FfnDesc, dict(C=320), "M"),
+        (lib.acth_layernorm, _lib.LayerNormDesc, dict(C=64), "M"),
+        (lib.acth_groupnorm, _lib.GroupNormDesc, dict(C=64, C1=64, G=32, rows_per_stat=16), "M"),
+        (lib.acth_mamba_combine_ln, _lib.MambaCombineDesc, dict(C=64, S=16), "M"),
+        (lib.acth_selective_scan, _lib.ScanDesc, dict(N=16, R=4, L=64, D=64, G=2), "nb"),
+        (lib.acth_conv_direct, _lib.ConvDirectDesc, dict(Cin=3, Cout=16, H=8, W=8), "B"),
+    ]
+    for fn, cls, fields, size in cases:
+        d = cls()
+        for k, v in fields.items():
+            setattr(d, k, v)
+        setattr(d, size, 0)
+        assert fn(ctypes.byref(d), None) == 0, (fn.__name__, size)
+        setattr(d, size, -1)
+        assert fn(ctypes.byref(d), None) == -1, (fn.__name__, size)
+    s0, s1 = _lib.ScanDesc(), _lib.ScanDesc()
+    assert lib.acth_selective_scan2(ctypes.byref(s0), ctypes.byref(s1), None) == 0
 
 
 def test_no_cpu_fallback():

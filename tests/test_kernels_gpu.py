@@ -873,3 +873,24 @@ def test_cfg_euler_accum_matches_reference_scheduler_mirror(dev):
         ops.cfg_euler_accum(noise, offs, lat, fidx, 0.0, 0.0, 0.0, sig[i], sig[i + 1], acc, cnt, F_, S)
         want = rows(g["prev"][i])
         torch.testing.assert_close(acc.cpu(), want, rtol=1e-5, atol=1e-5 * (1 + sig[i]))
+
+
+def test_empty_inputs_give_empty_outputs(dev):
+    """Zero rows / an empty batch through the ops and the selective_scan_fn drop-in: empty outputs of the right shape,
+    no launch (the C ABI's no-work rule, include/actalker_hip.h), as the torch ops they replace accept."""
+    from actalker_amd.selective_scan_interface import selective_scan_fn
+    dt = ops.act_dtype()
+    x = torch.empty(0, 64, device=dev, dtype=dt)
+    w = bf(rnd(32, 64)).to(dev)
+    assert ops.gemm(x, w).shape == (0, 32)
+    g, b = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    assert ops.layernorm(x, g, b, 1e-5).shape == (0, 64)
+    assert ops.groupnorm(x, g, b, 1e-6, 16, silu=True).shape == (0, 64)
+    assert ops.flash_attn(torch.empty(0, 3 * 64, device=dev, dtype=dt), 0, 16, 1).shape[0] == 0
+    u = torch.empty(0, 64, 12, device=dev, dtype=dt)
+    A = -torch.rand(64, 16, device=dev)
+    Bc = torch.empty(0, 2, 16, 12, device=dev, dtype=dt)
+    y = selective_scan_fn(u, u, A, Bc, Bc, D=torch.ones(64, device=dev), delta_bias=torch.zeros(64, device=dev),
+                          delta_softplus=True)
+    assert y.shape == (0, 64, 12)
+    torch.cuda.synchronize()

@@ -8,6 +8,10 @@ Shared by tools/gen_golden_unet_ref.py (case ``win14_mode0``: the REFERENCE UNet
 B = 3 x F = 14, inputs stacked as the reference pipeline stacks them at pipeline:712-729) and
 tests/test_full_geometry_gpu.py (the HIP backend's call on the same tensors, each unit held to its golden batch
 element).
+
+``mode=2`` (case ``win14_mode2``): the same window in mode 2, audio + expression (gate [1, 1]), the C4 / C5
+workload's call: all four CFG branches (uncond / drop audio+vasa / drop vasa / cond, pipeline:162-200, 192-201)
+with the masks [mouth, exp] (pipeline:703-704); no branch is a twin, branches 1-3 share the UNet prefix.
 """
 import math
 
@@ -18,26 +22,34 @@ H, W = H_PX // 8, W_PX // 8
 F = 14
 NB = 3                   # CFG branches of the window: 0 uncond, 1 drop audio+vasa, 2 drop vasa (cond audio)
 GATE = [1, 0]            # mode 0 (audio-only): VASA prompts gated to zero (pipeline:724)
+MODES = {0: dict(nb=3, gate=[1, 0]), 2: dict(nb=4, gate=[1, 1])}   # mode 2: + branch 3, cond (audio and VASA)
 SIGMA = 1.6555           # Karras step 12 of 25
 SEED = 17
 
 
-def loop_tensors(seed: int = SEED):
+def loop_tensors(seed: int = SEED, mode: int = 0):
     """The pipeline-internal tensors after CFG stacking (pipeline:128-205, 636-638) for one window of F frames:
     (lat (1, F, 4, h, w) noisy latents, imgl (NB, F, 4, h, w), ide (NB, F, 1, 1024), aud (NB, F, 32, 1024),
-    vas (NB, F, 1, 1024), pose (1, F, 320, h, w), added (NB, 3), masks (face, mouth, exp))."""
+    vas (NB, F, 1, 1024), pose (1, F, 320, h, w), added (NB, 3), masks (face, mouth, exp)). Mode 0's draws come
+    first in the same order for both modes (the mode-0 fixture's inputs checksum is unchanged)."""
+    nb = MODES[mode]["nb"]
     g = torch.Generator().manual_seed(seed)
     lat = SIGMA * torch.randn(1, F, 4, H, W, generator=g) + 0.18215 * torch.randn(1, 1, 4, H, W, generator=g)
     il = torch.randn(1, 1, 4, H, W, generator=g).expand(1, F, 4, H, W)
-    imgl = torch.cat([torch.zeros_like(il), il, il]).contiguous()
+    imgl = torch.cat([torch.zeros_like(il)] + [il] * (nb - 1)).contiguous()
     e = torch.randn(1, 1, 1, 1024, generator=g).expand(1, F, 1, 1024)
-    ide = torch.cat([torch.zeros_like(e), e, e]).contiguous()
+    ide = torch.cat([torch.zeros_like(e)] + [e] * (nb - 1)).contiguous()
     a_u, a_c = torch.randn(1, F, 32, 1024, generator=g), torch.randn(1, F, 32, 1024, generator=g)
-    aud = torch.cat([a_u, a_u, a_c]).contiguous()
     v_u = torch.randn(1, F, 1, 1024, generator=g)
-    vas = torch.cat([v_u, v_u, v_u]).contiguous()
     pose = 0.1 * torch.randn(1, F, 320, H, W, generator=g)
-    added = torch.tensor([[12.5, 12.0, 20.0]] * NB)
+    if nb == 3:
+        aud = torch.cat([a_u, a_u, a_c]).contiguous()
+        vas = torch.cat([v_u, v_u, v_u]).contiguous()
+    else:
+        v_c = torch.randn(1, F, 1, 1024, generator=g)
+        aud = torch.cat([a_u, a_u, a_c, a_c]).contiguous()
+        vas = torch.cat([v_u, v_u, v_u, v_c]).contiguous()
+    added = torch.tensor([[12.5, 12.0, 20.0]] * nb)
     face = torch.zeros(1, 1, H_PX, W_PX)
     face[..., H_PX // 4: 3 * H_PX // 4, 5 * W_PX // 16: 11 * W_PX // 16] = 1.0
     mouth = torch.zeros(1, 1, H_PX, W_PX)
@@ -45,14 +57,16 @@ def loop_tensors(seed: int = SEED):
     return lat, imgl, ide, aud, vas, pose, added, (face, mouth, 1.0 - mouth)
 
 
-def reference_inputs(seed: int = SEED):
+def reference_inputs(seed: int = SEED, mode: int = 0):
     """The reference pipeline's UNet call on these tensors (pipeline:712-729): scale_model_input (x / sqrt(sigma^2
     + 1)), image latents concatenated on channels, prompts flattened and gated, pose repeated per branch, the
-    gate's masks [face, 0] (pipeline:702-711). Returns (sample, t, ehs, added, pose, masks)."""
-    lat, imgl, ide, aud, vas, pose, added, (face, mouth, exp) = loop_tensors(seed)
-    x = (lat / math.sqrt(SIGMA * SIGMA + 1.0)).repeat(NB, 1, 1, 1, 1)
+    gate's masks (pipeline:702-711: mode 0 [face, 0], mode 2 [mouth, exp]). Returns (sample, t, ehs, added, pose,
+    masks)."""
+    nb, gate = MODES[mode]["nb"], MODES[mode]["gate"]
+    lat, imgl, ide, aud, vas, pose, added, (face, mouth, exp) = loop_tensors(seed, mode)
+    x = (lat / math.sqrt(SIGMA * SIGMA + 1.0)).repeat(nb, 1, 1, 1, 1)
     sample = torch.cat([x, imgl], dim=2)
     t = torch.tensor(0.25 * math.log(SIGMA))
-    ehs = (ide.flatten(0, 1), [aud.flatten(0, 1) * GATE[0], vas.flatten(0, 1) * GATE[1]])
-    masks = [face, torch.zeros_like(face)]
-    return sample, t, ehs, added, pose.repeat(NB, 1, 1, 1, 1), masks
+    ehs = (ide.flatten(0, 1), [aud.flatten(0, 1) * gate[0], vas.flatten(0, 1) * gate[1]])
+    masks = [face, torch.zeros_like(face)] if mode == 0 else [mouth, exp]
+    return sample, t, ehs, added, pose.repeat(nb, 1, 1, 1, 1), masks

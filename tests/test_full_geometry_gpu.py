@@ -361,54 +361,61 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case, act):
 
 
 # ------------------------------------------------------------------------------------------ headline window call
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("act", ["bf16", "fp16"])
-def test_headline_window_call_matches_reference_run(dev, full_unet, act):
+def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode):
     """The call the headline times, held to the REFERENCE UNet run at that shape: one
-    14-frame window at 576x1024, its three mode-0 CFG branches (uncond / drop audio+vasa / drop vasa) as three units
+    14-frame window at 576x1024, its mode-0 CFG branches (uncond / drop audio+vasa / drop vasa) as three units
     of ONE HipBackend.run_units call -- window-input scaling, the CFG prefix shared by branches 1 and 2, the batched
     per-call context projections, automatic units per call -- against tools/gen_golden_unet_ref.py's
     ``win14_mode0`` (the reference UNet package by path, B = 3 x F = 14, inputs stacked as pipeline:712-729 does).
+    ``mode`` 2: the C4 / C5 workload's call, all four branches (no twin; branches 1-3 share the prefix) with the
+    masks [mouth, exp], against ``win14_mode2``.
     Stated tolerance per unit: 1.5x the bf16 (fp16) rounding floor the oracle shows at this geometry and weights
-    (tests/golden/unet_full_mode0_rounded.safetensors: every op's inputs / outputs rounded at its boundary), capped
-    at 2e-2 as every UNet golden; max |err| < 0.25 x output rms."""
+    (tests/golden/unet_full_mode0_rounded.safetensors for mode 0, unet_full_half_rounded.safetensors -- the same
+    [lower, upper] mask split with both prompts live -- for mode 2: every op's inputs / outputs rounded at its
+    boundary), capped at 2e-2 as every UNet golden; max |err| < 0.25 x output rms."""
     from actalker_amd import pipeline as pl
     from tests import golden_win14 as gw
-    path = os.path.join(GOLD, "unet_ref_win14_mode0.safetensors")
+    case = f"win14_mode{mode}"
+    path = os.path.join(GOLD, f"unet_ref_{case}.safetensors")
     if not os.path.exists(path):
-        pytest.skip("headline-window reference fixture not generated (tools/gen_golden_unet_ref.py win14_mode0)")
+        pytest.skip(f"headline-window reference fixture not generated (tools/gen_golden_unet_ref.py {case})")
     g = load_file(path)
     unet, wsum = full_unet
     torch.testing.assert_close(wsum, g["weights_checksum"], rtol=1e-6, atol=1e-6)
-    sample, t, ehs, added_r, pose_r, masks_r = gw.reference_inputs()
+    sample, t, ehs, added_r, pose_r, masks_r = gw.reference_inputs(mode=mode)
     torch.testing.assert_close(gf.checksum(sample, ehs[0], *ehs[1], pose_r, *masks_r), g["inputs_checksum"],
                                rtol=1e-6, atol=1e-6)
-    lat, imgl, ide, aud, vas, pose, added, masks = gw.loop_tensors()
-    floor = load_file(os.path.join(GOLD, "unet_full_mode0_rounded.safetensors"))
-    full = load_file(os.path.join(GOLD, "unet_full_mode0.safetensors"))["out"]
+    nb, gate = gw.MODES[mode]["nb"], gw.MODES[mode]["gate"]
+    lat, imgl, ide, aud, vas, pose, added, masks = gw.loop_tensors(mode=mode)
+    fcase = "mode0" if mode == 0 else "half"
+    floor = load_file(os.path.join(GOLD, f"unet_full_{fcase}_rounded.safetensors"))
+    full = load_file(os.path.join(GOLD, f"unet_full_{fcase}.safetensors"))["out"]
     fl = _stats(floor["fp16" if act == "fp16" else "bf16"], full)["rel_l2"]
     tol = min(2e-2, 1.5 * fl)
     unet.acth_compute_dtype = torch.float16 if act == "fp16" else torch.bfloat16
     try:
-        be = pl.HipBackend(unet, gw.H, gw.W, masks, gw.GATE, added, gw.F, gw.F, imgl, ide, aud, vas, pose)
-        assert be.max_units_per_call() >= gw.NB              # one call, as the bench's auto split gives
-        assert be.prefix_classes() == [0, 1, 1]              # branches 1 and 2 share the UNet prefix
+        be = pl.HipBackend(unet, gw.H, gw.W, masks, gate, added, gw.F, gw.F, imgl, ide, aud, vas, pose)
+        assert be.max_units_per_call() >= nb                 # one call, as the bench's auto split gives
+        assert be.prefix_classes() == [0] + [1] * (nb - 1)   # branches 1.. share the UNet prefix
         assert be.branch_twins() == {}
         frames = [list(range(gw.F))]
         state = be.new_state(lat)
         S = gw.H * gw.W
-        out = torch.empty((gw.NB * gw.F * S, 4), device=dev, dtype=torch.float32)
+        out = torch.empty((nb * gw.F * S, 4), device=dev, dtype=torch.float32)
         be.begin_step(frames)
         with torch.no_grad():
-            be.run_units(state, [(0, c) for c in range(gw.NB)], frames, float(t), gw.SIGMA, out, 0)
+            be.run_units(state, [(0, c) for c in range(nb)], frames, float(t), gw.SIGMA, out, 0)
         torch.cuda.synchronize()
     finally:
         unet.acth_compute_dtype = None
-    got = out.view(gw.NB, gw.F, gw.H, gw.W, 4).permute(0, 1, 4, 2, 3)
+    got = out.view(nb, gw.F, gw.H, gw.W, 4).permute(0, 1, 4, 2, 3)
     want = g["out"]
-    for c in range(gw.NB):
+    for c in range(nb):
         st = _stats(got[c], want[c])
         st["rounding_floor_rel_l2"] = fl
-        _log(f"win14_mode0_unit{c}_{act}", st)
+        _log(f"{case}_unit{c}_{act}", st)
         assert torch.isfinite(got[c]).all()
         assert st["rel_l2"] < tol, (c, st)
         assert st["max_abs"] < 0.25 * st["ref_rms"], (c, st)

@@ -61,10 +61,24 @@ def main(cases):
         isum = gf.checksum(sample, ehs[0], *ehs[1], pose, *masks)
         # the reference mutates the ip_hidden_states list in place (attention_processor.py:2842-2843): hand it
         # its own list
-        ref_ehs = (ehs[0].clone(), [e.clone() for e in ehs[1]])
         t0 = time.time()
-        out = unet(sample, t, ref_ehs, added, spatial_condition=pose,
-                   cross_attention_kwargs={"ip_adapter_masks": [m.clone() for m in masks]}, return_dict=False)[0]
+        if case in gu.PER_ELEMENT:
+            # one batch element per reference forward (the UNet treats batch elements independently: GroupNorm,
+            # attention and the scans are per element), concatenated along the batch
+            B, F = sample.shape[:2]
+            outs = []
+            for b in range(B):
+                fs = slice(b * F, (b + 1) * F)
+                ref_ehs = (ehs[0][fs].clone(), [e[fs].clone() for e in ehs[1]])
+                outs.append(unet(sample[b:b + 1], t, ref_ehs, added[b:b + 1], spatial_condition=pose[b:b + 1],
+                                 cross_attention_kwargs={"ip_adapter_masks": [m.clone() for m in masks]},
+                                 return_dict=False)[0])
+                print(f"{case}: element {b} done at {time.time() - t0:.0f}s", flush=True)
+            out = torch.cat(outs)
+        else:
+            ref_ehs = (ehs[0].clone(), [e.clone() for e in ehs[1]])
+            out = unet(sample, t, ref_ehs, added, spatial_condition=pose,
+                       cross_attention_kwargs={"ip_adapter_masks": [m.clone() for m in masks]}, return_dict=False)[0]
         dt = time.time() - t0
         print(f"{case}: reference forward {dt:.1f}s, out {tuple(out.shape)} rms {out.pow(2).mean().sqrt():.4f}",
               flush=True)

@@ -9,6 +9,9 @@ B = 3 x F = 14, inputs stacked as the reference pipeline stacks them at pipeline
 tests/test_full_geometry_gpu.py (the HIP backend's call on the same tensors, each unit held to its golden batch
 element).
 
+``mode=1`` (case ``win14_mode1``): expression-only (gate [0, 1], masks [0, face]); branch 2's inputs equal branch 1's
+bitwise once the audio prompts are gated, so the reference is run for the distinct branches 0, 1, 3 (the HIP
+backend's twin elimination evaluates the same three).
 ``mode=2`` (case ``win14_mode2``): the same window in mode 2, audio + expression (gate [1, 1]), the C4 / C5
 workload's call: all four CFG branches (uncond / drop audio+vasa / drop vasa / cond, pipeline:162-200, 192-201)
 with the masks [mouth, exp] (pipeline:703-704); no branch is a twin, branches 1-3 share the UNet prefix.
@@ -22,7 +25,9 @@ H, W = H_PX // 8, W_PX // 8
 F = 14
 NB = 3                   # CFG branches of the window: 0 uncond, 1 drop audio+vasa, 2 drop vasa (cond audio)
 GATE = [1, 0]            # mode 0 (audio-only): VASA prompts gated to zero (pipeline:724)
-MODES = {0: dict(nb=3, gate=[1, 0]), 2: dict(nb=4, gate=[1, 1])}   # mode 2: + branch 3, cond (audio and VASA)
+MODES = {0: dict(nb=3, gate=[1, 0]), 1: dict(nb=4, gate=[0, 1]), 2: dict(nb=4, gate=[1, 1])}
+# mode 2: + branch 3, cond (audio and VASA); mode 1 (expression-only): audio gated to zero, so branch 2 (drop vasa)
+# is bitwise branch 1 (drop audio+vasa) and the distinct branches are 0, 1, 3
 SIGMA = 1.6555           # Karras step 12 of 25
 SEED = 17
 
@@ -60,7 +65,7 @@ def loop_tensors(seed: int = SEED, mode: int = 0):
 def reference_inputs(seed: int = SEED, mode: int = 0):
     """The reference pipeline's UNet call on these tensors (pipeline:712-729): scale_model_input (x / sqrt(sigma^2
     + 1)), image latents concatenated on channels, prompts flattened and gated, pose repeated per branch, the
-    gate's masks (pipeline:702-711: mode 0 [face, 0], mode 2 [mouth, exp]). Returns (sample, t, ehs, added, pose,
+    gate's masks (pipeline:702-711: mode 0 [face, 0], mode 1 [0, face], mode 2 [mouth, exp]). Returns (sample, t, ehs, added, pose,
     masks)."""
     nb, gate = MODES[mode]["nb"], MODES[mode]["gate"]
     lat, imgl, ide, aud, vas, pose, added, (face, mouth, exp) = loop_tensors(seed, mode)
@@ -68,5 +73,5 @@ def reference_inputs(seed: int = SEED, mode: int = 0):
     sample = torch.cat([x, imgl], dim=2)
     t = torch.tensor(0.25 * math.log(SIGMA))
     ehs = (ide.flatten(0, 1), [aud.flatten(0, 1) * gate[0], vas.flatten(0, 1) * gate[1]])
-    masks = [face, torch.zeros_like(face)] if mode == 0 else [mouth, exp]
+    masks = {0: [face, torch.zeros_like(face)], 1: [torch.zeros_like(face), face], 2: [mouth, exp]}[mode]
     return sample, t, ehs, added, pose.repeat(nb, 1, 1, 1, 1), masks

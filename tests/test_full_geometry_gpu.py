@@ -361,7 +361,7 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case, act):
 
 
 # ------------------------------------------------------------------------------------------ headline window call
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("act", ["bf16", "fp16"])
 def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode):
     """The call the headline times, held to the REFERENCE UNet run at that shape: one
@@ -370,7 +370,8 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode):
     per-call context projections, automatic units per call -- against tools/gen_golden_unet_ref.py's
     ``win14_mode0`` (the reference UNet package by path, B = 3 x F = 14, inputs stacked as pipeline:712-729 does).
     ``mode`` 2: the C4 / C5 workload's call, all four branches (no twin; branches 1-3 share the prefix) with the
-    masks [mouth, exp], against ``win14_mode2``.
+    masks [mouth, exp], against ``win14_mode2``. ``mode`` 1 (expression-only): branch 2 is branch 1's twin, so the
+    call evaluates branches 0, 1, 3, against ``win14_mode1`` (the reference run for those three).
     Stated tolerance per unit: 1.5x the bf16 (fp16) rounding floor the oracle shows at this geometry and weights
     (tests/golden/unet_full_mode0_rounded.safetensors for mode 0, unet_full_half_rounded.safetensors -- the same
     [lower, upper] mask split with both prompts live -- for mode 2: every op's inputs / outputs rounded at its
@@ -389,7 +390,7 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode):
                                rtol=1e-6, atol=1e-6)
     nb, gate = gw.MODES[mode]["nb"], gw.MODES[mode]["gate"]
     lat, imgl, ide, aud, vas, pose, added, masks = gw.loop_tensors(mode=mode)
-    fcase = "mode0" if mode == 0 else "half"
+    fcase = "half" if mode == 2 else "mode0"
     floor = load_file(os.path.join(GOLD, f"unet_full_{fcase}_rounded.safetensors"))
     full = load_file(os.path.join(GOLD, f"unet_full_{fcase}.safetensors"))["out"]
     fl = _stats(floor["fp16" if act == "fp16" else "bf16"], full)["rel_l2"]
@@ -399,23 +400,26 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode):
         be = pl.HipBackend(unet, gw.H, gw.W, masks, gate, added, gw.F, gw.F, imgl, ide, aud, vas, pose)
         assert be.max_units_per_call() >= nb                 # one call, as the bench's auto split gives
         assert be.prefix_classes() == [0] + [1] * (nb - 1)   # branches 1.. share the UNet prefix
-        assert be.branch_twins() == {}
+        twins = {2: 1} if mode == 1 else {}
+        assert be.branch_twins() == twins
+        branches = [c for c in range(nb) if c not in twins]
         frames = [list(range(gw.F))]
         state = be.new_state(lat)
         S = gw.H * gw.W
-        out = torch.empty((nb * gw.F * S, 4), device=dev, dtype=torch.float32)
+        out = torch.empty((len(branches) * gw.F * S, 4), device=dev, dtype=torch.float32)
         be.begin_step(frames)
         with torch.no_grad():
-            be.run_units(state, [(0, c) for c in range(nb)], frames, float(t), gw.SIGMA, out, 0)
+            be.run_units(state, [(0, c) for c in branches], frames, float(t), gw.SIGMA, out, 0)
         torch.cuda.synchronize()
     finally:
         unet.acth_compute_dtype = None
-    got = out.view(nb, gw.F, gw.H, gw.W, 4).permute(0, 1, 4, 2, 3)
-    want = g["out"]
-    for c in range(nb):
+    got = out.view(len(branches), gw.F, gw.H, gw.W, 4).permute(0, 1, 4, 2, 3)
+    want = g["out"]                        # the reference run's elements, in the same order as ``branches``
+    assert want.shape[0] == len(branches)
+    for c in range(len(branches)):
         st = _stats(got[c], want[c])
         st["rounding_floor_rel_l2"] = fl
-        _log(f"{case}_unit{c}_{act}", st)
+        _log(f"{case}_unit{branches[c]}_{act}", st)
         assert torch.isfinite(got[c]).all()
         assert st["rel_l2"] < tol, (c, st)
         assert st["max_abs"] < 0.25 * st["ref_rms"], (c, st)

@@ -67,14 +67,14 @@ def main(cases):
             # attention and the scans are per element), concatenated along the batch
             B, F = sample.shape[:2]
             outs = []
-            for b in range(B):
+            for b in gu.ELEMENTS.get(case, range(B)):
                 fs = slice(b * F, (b + 1) * F)
                 ref_ehs = (ehs[0][fs].clone(), [e[fs].clone() for e in ehs[1]])
                 outs.append(unet(sample[b:b + 1], t, ref_ehs, added[b:b + 1], spatial_condition=pose[b:b + 1],
                                  cross_attention_kwargs={"ip_adapter_masks": [m.clone() for m in masks]},
                                  return_dict=False)[0])
                 print(f"{case}: element {b} done at {time.time() - t0:.0f}s", flush=True)
-            out = torch.cat(outs)
+            out = torch.cat(outs)          # the elements run, in order (gu.ELEMENTS)
         else:
             ref_ehs = (ehs[0].clone(), [e.clone() for e in ehs[1]])
             out = unet(sample, t, ref_ehs, added, spatial_condition=pose,

@@ -29,6 +29,7 @@ and mamba-ssm's selective_scan_ref are restatements.
   the distinct branches 0, 1, 3 (branch 2's gated inputs are bitwise branch 1's), batch-1 forwards.
 * ``win25_mode0``: the mode-0 window at the reference's shipped length, F = 25 (config/inference.yaml:4), 576x1024,
   B = 3 CFG branches, batch-1 forwards.
+* ``c1win14_mode0``: the mode-0 window call at BASELINE C1's geometry, 576x576, F = 14, B = 3, batch-1 forwards.
 * ``c1_face0``: the same UNet at BASELINE C1's geometry, 576x576 (latent 72x72; levels 72x72 / 36x36 / 18x18 /
   9x9), B = 1 x F = 2, mode 0 (gate [1, 0], zero VASA tokens) with a centre face box as the audio mask.
 
@@ -49,8 +50,9 @@ TINY_CASES = ("tiny_mode0", "tiny_mode1", "tiny_mode2", "tiny_half", "tiny_box",
 # so every temporal block (attention.py:431-433, the temporal ResBlocks' (3,1,1) convs and GroupNorm) spans 25 frames
 F25 = 25
 FULL_CASES = ("full_half", "full_mode0", "full_mode2", "c1_face0", "win14_mode0", "win14_mode1", "win14_mode2",
-              "win25_mode0")
-PER_ELEMENT = ("win14_mode1", "win14_mode2", "win25_mode0")   # reference forward run one batch element at a time
+              "win25_mode0", "c1win14_mode0")
+# reference forward run one batch element at a time
+PER_ELEMENT = ("win14_mode1", "win14_mode2", "win25_mode0", "c1win14_mode0")
 # batch elements a per-element case runs (default: all); win14_mode1's element 2 is bitwise element 1's input
 ELEMENTS = {"win14_mode1": (0, 1, 3)}
 CASES = TINY_CASES + FULL_CASES
@@ -103,6 +105,9 @@ def case_inputs(case: str):
     if case.startswith("win14_mode") or case.startswith("win25_mode"):
         from tests import golden_win14 as gw
         return gw.reference_inputs(mode=int(case[-1]), frames=int(case[3:5]))
+    if case == "c1win14_mode0":
+        from tests import golden_win14 as gw
+        return gw.reference_inputs(mode=0, frames=14, w_px=576)
     raise ValueError(case)
 
 

@@ -11,6 +11,7 @@ element).
 
 ``frames=25`` (case ``win25_mode0``): the reference's shipped window, n_sample_frames = 25 (config/inference.yaml:4 ->
 Inference.py:573 frames_per_batch), mode 0, at the real widths: the temporal attention spans two 16-frame MFMA blocks.
+``w_px=576`` (case ``c1win14_mode0``): BASELINE C1's geometry, 576x576 (latent 72x72), the same mode-0 window.
 ``mode=1`` (case ``win14_mode1``): expression-only (gate [0, 1], masks [0, face]); branch 2's inputs equal branch 1's
 bitwise once the audio prompts are gated, so the reference is run for the distinct branches 0, 1, 3 (the HIP
 backend's twin elimination evaluates the same three).
@@ -34,13 +35,15 @@ SIGMA = 1.6555           # Karras step 12 of 25
 SEED = 17
 
 
-def loop_tensors(seed: int = SEED, mode: int = 0, frames: int = F):
+def loop_tensors(seed: int = SEED, mode: int = 0, frames: int = F, w_px: int = W_PX):
     """The pipeline-internal tensors after CFG stacking (pipeline:128-205, 636-638) for one window of F frames:
     (lat (1, F, 4, h, w) noisy latents, imgl (NB, F, 4, h, w), ide (NB, F, 1, 1024), aud (NB, F, 32, 1024),
     vas (NB, F, 1, 1024), pose (1, F, 320, h, w), added (NB, 3), masks (face, mouth, exp)). Mode 0's draws come
     first in the same order for both modes (the mode-0 fixture's inputs checksum is unchanged)."""
     nb = MODES[mode]["nb"]
     F = frames
+    H_PX, W_PX = globals()["H_PX"], w_px
+    H, W = H_PX // 8, W_PX // 8
     g = torch.Generator().manual_seed(seed)
     lat = SIGMA * torch.randn(1, F, 4, H, W, generator=g) + 0.18215 * torch.randn(1, 1, 4, H, W, generator=g)
     il = torch.randn(1, 1, 4, H, W, generator=g).expand(1, F, 4, H, W)
@@ -65,13 +68,13 @@ def loop_tensors(seed: int = SEED, mode: int = 0, frames: int = F):
     return lat, imgl, ide, aud, vas, pose, added, (face, mouth, 1.0 - mouth)
 
 
-def reference_inputs(seed: int = SEED, mode: int = 0, frames: int = F):
+def reference_inputs(seed: int = SEED, mode: int = 0, frames: int = F, w_px: int = W_PX):
     """The reference pipeline's UNet call on these tensors (pipeline:712-729): scale_model_input (x / sqrt(sigma^2
     + 1)), image latents concatenated on channels, prompts flattened and gated, pose repeated per branch, the
     gate's masks (pipeline:702-711: mode 0 [face, 0], mode 1 [0, face], mode 2 [mouth, exp]). Returns (sample, t, ehs, added, pose,
     masks)."""
     nb, gate = MODES[mode]["nb"], MODES[mode]["gate"]
-    lat, imgl, ide, aud, vas, pose, added, (face, mouth, exp) = loop_tensors(seed, mode, frames)
+    lat, imgl, ide, aud, vas, pose, added, (face, mouth, exp) = loop_tensors(seed, mode, frames, w_px)
     x = (lat / math.sqrt(SIGMA * SIGMA + 1.0)).repeat(nb, 1, 1, 1, 1)
     sample = torch.cat([x, imgl], dim=2)
     t = torch.tensor(0.25 * math.log(SIGMA))

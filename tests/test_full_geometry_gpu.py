@@ -361,9 +361,9 @@ def test_pipeline_call_matches_reference_pipeline_run(dev, case, act):
 
 
 # ------------------------------------------------------------------------------------------ headline window call
-@pytest.mark.parametrize("mode,frames", [(0, 14), (1, 14), (2, 14), (0, 25)])
+@pytest.mark.parametrize("mode,frames,w_px", [(0, 14, 1024), (1, 14, 1024), (2, 14, 1024), (0, 25, 1024), (0, 14, 576)])
 @pytest.mark.parametrize("act", ["bf16", "fp16"])
-def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, frames):
+def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, frames, w_px):
     """The call the headline times, held to the REFERENCE UNet run at that shape: one
     14-frame window at 576x1024, its mode-0 CFG branches (uncond / drop audio+vasa / drop vasa) as three units
     of ONE HipBackend.run_units call -- window-input scaling, the CFG prefix shared by branches 1 and 2, the batched
@@ -373,25 +373,27 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
     masks [mouth, exp], against ``win14_mode2``. ``mode`` 1 (expression-only): branch 2 is branch 1's twin, so the
     call evaluates branches 0, 1, 3, against ``win14_mode1`` (the reference run for those three). ``frames`` 25: the
     reference's shipped window (config/inference.yaml:4 n_sample_frames) at 576x1024, mode 0, against ``win25_mode0``:
-    the temporal attention's two-block (F <= 32) kernel at the real widths.
+    the temporal attention's two-block (F <= 32) kernel at the real widths. ``w_px`` 576: BASELINE C1's geometry
+    (576x576), mode 0, against ``c1win14_mode0`` (floor: the 576x1024 mode-0 one).
     Stated tolerance per unit: 1.5x the bf16 (fp16) rounding floor the oracle shows at this geometry and weights
     (tests/golden/unet_full_mode0_rounded.safetensors for mode 0, unet_full_half_rounded.safetensors -- the same
     [lower, upper] mask split with both prompts live -- for mode 2: every op's inputs / outputs rounded at its
     boundary), capped at 2e-2 as every UNet golden; max |err| < 0.25 x output rms."""
     from actalker_amd import pipeline as pl
     from tests import golden_win14 as gw
-    case = f"win{frames}_mode{mode}"
+    case = f"win{frames}_mode{mode}" if w_px == 1024 else f"c1win{frames}_mode{mode}"
+    H, W = gw.H_PX // 8, w_px // 8
     path = os.path.join(GOLD, f"unet_ref_{case}.safetensors")
     if not os.path.exists(path):
         pytest.skip(f"headline-window reference fixture not generated (tools/gen_golden_unet_ref.py {case})")
     g = load_file(path)
     unet, wsum = full_unet
     torch.testing.assert_close(wsum, g["weights_checksum"], rtol=1e-6, atol=1e-6)
-    sample, t, ehs, added_r, pose_r, masks_r = gw.reference_inputs(mode=mode, frames=frames)
+    sample, t, ehs, added_r, pose_r, masks_r = gw.reference_inputs(mode=mode, frames=frames, w_px=w_px)
     torch.testing.assert_close(gf.checksum(sample, ehs[0], *ehs[1], pose_r, *masks_r), g["inputs_checksum"],
                                rtol=1e-6, atol=1e-6)
     nb, gate = gw.MODES[mode]["nb"], gw.MODES[mode]["gate"]
-    lat, imgl, ide, aud, vas, pose, added, masks = gw.loop_tensors(mode=mode, frames=frames)
+    lat, imgl, ide, aud, vas, pose, added, masks = gw.loop_tensors(mode=mode, frames=frames, w_px=w_px)
     fcase = "half" if mode == 2 else "mode0"
     floor = load_file(os.path.join(GOLD, f"unet_full_{fcase}_rounded.safetensors"))
     full = load_file(os.path.join(GOLD, f"unet_full_{fcase}.safetensors"))["out"]
@@ -399,7 +401,7 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
     tol = min(2e-2, 1.5 * fl)
     unet.acth_compute_dtype = torch.float16 if act == "fp16" else torch.bfloat16
     try:
-        be = pl.HipBackend(unet, gw.H, gw.W, masks, gate, added, frames, frames, imgl, ide, aud, vas, pose)
+        be = pl.HipBackend(unet, H, W, masks, gate, added, frames, frames, imgl, ide, aud, vas, pose)
         assert be.max_units_per_call() >= nb                 # one call, as the bench's auto split gives
         assert be.prefix_classes() == [0] + [1] * (nb - 1)   # branches 1.. share the UNet prefix
         twins = {2: 1} if mode == 1 else {}
@@ -407,7 +409,7 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
         branches = [c for c in range(nb) if c not in twins]
         win = [list(range(frames))]
         state = be.new_state(lat)
-        S = gw.H * gw.W
+        S = H * W
         out = torch.empty((len(branches) * frames * S, 4), device=dev, dtype=torch.float32)
         be.begin_step(win)
         with torch.no_grad():
@@ -415,7 +417,7 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
         torch.cuda.synchronize()
     finally:
         unet.acth_compute_dtype = None
-    got = out.view(len(branches), frames, gw.H, gw.W, 4).permute(0, 1, 4, 2, 3)
+    got = out.view(len(branches), frames, H, W, 4).permute(0, 1, 4, 2, 3)
     want = g["out"]                        # the reference run's elements, in the same order as ``branches``
     assert want.shape[0] == len(branches)
     for c in range(len(branches)):

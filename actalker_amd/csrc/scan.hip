@@ -246,8 +246,11 @@ __device__ __forceinline__ float pair_swap(float v) {
 // XB: xdbl rows in bf16 ([dt (R4) | B | C] per direction, the reference's x_dbl dtype), staged to fp32 in LDS;
 // the grid is then 1-D and dealt XCD-major (the channel blocks of one (batch, direction) share an L2), and the
 // forward direction stops at n_keep.
+// Occupancy: 4 waves per SIMD (128 VGPRs) for R <= 20, and for the bf16-row form at R = 40 (level 1: 6720 waves
+// take two rounds of 4096 slots instead of three of 3072; 1.98 vs 2.08-2.15 ms, the paired launch 3.52-3.56 vs
+// 3.74-3.76 ms, profiles/r5_scan_occupancy_ab.log); R = 80 stays at 3 (4 spills 21 VGPRs and measured slower)
 template <int R, int CH, bool SOFTPLUS, bool XB = false>
-__global__ __launch_bounds__(2 * CH, R <= 20 ? 4 : 3) void scan_pair_kernel(const ActhScanDesc p0,
+__global__ __launch_bounds__(2 * CH, (R <= 20 || (XB && R <= 40)) ? 4 : 3) void scan_pair_kernel(const ActhScanDesc p0,
                                                                              const ActhScanDesc p1, int nb0) {
   int bxi = blockIdx.x, kyi = blockIdx.y, bzi = blockIdx.z;
   if constexpr (XB) {

@@ -33,6 +33,9 @@ using namespace gemm;
 #define G8_CONV_CMAJOR 0
 #endif
 // 1: 3x3-conv rows (no upsample) carry their tap-(0, 0) pixel and a 9-bit in-image tap mask
+#ifndef G8_RING_STAMPS
+#define G8_RING_STAMPS 0      // 1: diagnostic build, per-wave segment cycle sums of the ring loop (tile bit 0x400)
+#endif
 #ifndef G8_TAP_MASK
 #define G8_TAP_MASK 1
 #endif
@@ -131,7 +134,9 @@ __device__ unsigned long long g_gemm_stamps[STAMP_WGS * 4];
 // four consecutive columns of one row (used by the GEGLU launches, whose gated outputs then leave straight from
 // registers); TR = false keeps four consecutive rows of one column, which the slab-based epilogues write out
 // marginally faster (the convs measured 2-5 % slower transposed, profiles/r3_step24_*).
-template <int BN_, int AMODE, bool TR = false>
+// RING: the main loop as a 4-slot ring of 32-deep sub-tiles (see the ring branch below) instead of the
+// 4-phase-per-64-deep-K-tile schedule; same LDS bytes, same epilogue.
+template <int BN_, int AMODE, bool TR = false, bool RING = true>
 __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, unsigned a_bytes, unsigned a2_bytes,
                                                         unsigned b_bytes, int vec_ok) {
   constexpr int WR = BN_ == 256 ? 2 : 4, WC = 8 / WR;
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const int stamp_wg = blockIdx.x + gridDim.x * blockIdx.y;
   const bool rt = (p.tile & 0x800) != 0;          // stamps from the 100 MHz real-time counter (chip-wide timeline)
   auto stamp = [&](int k) {
-    if (stamps && tid == 0 && stamp_wg < STAMP_WGS)
+    if (!G8_RING_STAMPS && stamps && tid == 0 && stamp_wg < STAMP_WGS)
       g_gemm_stamps[stamp_wg * 4 + k] = rt ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
   };
   stamp(0);
@@ -198,110 +203,9 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
   const __amdgpu_buffer_rsrc_t ra2 = make_rsrc(p.A2 ? p.A2 : p.A, p.A2 ? a2_bytes : 0u);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
-
-  // DMA: half-tile piece i (0..15) = rows [8i, 8i+8); wave w issues pieces w and w + 8.
-  // Lane -> (row 8i + lane/8, physical 16-B slot lane%8) holding logical K chunk slot ^ (row & 7).
-  const int lrow = lane >> 3;
-  const int cch = (lane & 7) ^ lrow;
-  // rows [h][u]: half h, piece w + 8u
-  RowPk rp[2][2];
-  unsigned aoff[2][2], aoff2[2][2], boff[2][NBJ];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      rp[h][u] = pack_row<AMODE>(p, tile_m + h * 128 + (wave + 8 * u) * 8 + lrow);
-    }
-#pragma unroll
-    for (int u = 0; u < NBJ; ++u) {
-      const int brow = tile_n + h * (BN_ / 2) + (wave + 8 * u) * 8 + lrow;
-      boff[h][u] = brow < p.N ? ((unsigned)brow * p.ldb + cch * 8) * 2u : OOB;
-    }
-  }
-  auto set_tap = [&](int tap) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int pix = tap_pixel8<AMODE>(p, rp[h][u], tap);
-        aoff[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda + cch * 8) * 2u;
-        aoff2[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda2 + cch * 8) * 2u;
-      }
-  };
-  set_tap(0);
   const bool two_src = p.A2 != nullptr;
   const int cin = AMODE == 0 ? 0x7fffffff : p.Cin;
-  const int nk = (p.K + 63) / 64;
-  const int kfull = p.K / 64;
-
-  // per-K-tile staging parameters, advanced by prep_k() in K order
-  int s_tap = 0, s_c0 = 0, s_ky = 0, s_kx = 0;
-  int k_c0 = 0, k_k0 = 0, k_kb = 0;
-  bool k_second = false, k_tail = false;
-  const int ntap = AMODE == 0 ? 1 : p.K / cin;
-  auto prep_k = [&](int kt) {
-    k_k0 = kt * 64;
-    k_kb = k_k0;
-    if (AMODE == 0) {
-      k_c0 = k_k0;
-    } else if (AMODE == 1 && G8_CONV_CMAJOR == 2) {
-      // (ky, 64-channel slice, kx): the three kx taps of a slice -- the same image pixels shifted by one --
-      // are consecutive K tiles, so their re-reads meet in L2 one K tile apart instead of a channel pass apart
-      const int tap = s_ky * 3 + s_kx;
-      set_tap(tap);
-      k_c0 = s_c0;
-      k_kb = tap * cin + s_c0;
-      if (++s_kx == 3) {
-        s_kx = 0;
-        s_c0 += 64;
-        if (s_c0 == cin) { s_c0 = 0; ++s_ky; }
-      }
-    } else if (AMODE == 1 && G8_CONV_CMAJOR == 1) {
-      // 3x3 conv, 64-channel slice outer and tap inner: the nine taps of one slice read one ~4-image-row
-      // window of it in consecutive K tiles, so the window stays in L2 (tap-major order re-reads every
-      // input row from HBM once per tap row: 4.3 GB per level-0 conv dispatch for ~1.5 GB of operands).
-      // B's K offset follows (K index tap * Cin + c)
-      set_tap(s_tap);
-      k_c0 = s_c0;
-      k_kb = s_tap * cin + s_c0;
-      if (++s_tap == ntap) { s_tap = 0; s_c0 += 64; }
-    } else {
-      if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
-      k_c0 = s_c0;
-      s_c0 += 64;
-      if (s_c0 == cin) { s_c0 = 0; ++s_tap; }
-    }
-    k_second = two_src && k_c0 >= p.K1;
-    k_tail = kt >= kfull;
-  };
-  auto stage_a = [&](int h, int buf) {
-    char* dst0 = smem + buf * BUF + h * AH;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      unsigned off = k_second ? aoff2[h][u] + (unsigned)(k_c0 - p.K1) * 2u : aoff[h][u] + (unsigned)k_c0 * 2u;
-      if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
-      lds_void* dst = (lds_void*)(dst0 + (wave + 8 * u) * 1024);
-      if (k_second) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra2, dst, 16, off, 0, 0, 0);
-      else __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, off, 0, 0, 0);
-    }
-  };
-  auto stage_b = [&](int h, int buf) {
-    char* dst0 = smem + buf * BUF + 2 * AH + h * BH;
-#pragma unroll
-    for (int u = 0; u < NBJ; ++u) {
-      if (NBP % 8 == 0 || wave + 8 * u < NBP) {
-        unsigned off = boff[h][u] + (unsigned)k_kb * 2u;
-        if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + (wave + 8 * u) * 1024), 16, off, 0, 0, 0);
-      }
-    }
-  };
-
-  // fragment reads: row base + 16 t + lane%16, swizzle key row & 7 == lane & 7
-  const int fr = lane & 15, fkey = lane & 7, fq = lane >> 4;
-  const int sw0 = ((0 + fq) ^ fkey) << 4, sw1 = ((4 + fq) ^ fkey) << 4;
-  const int a_row = (wr * TMQ * 16 + fr) * 128;   // inside an A half
-  const int b_row = (wc * TNQ * 16 + fr) * 128;   // inside a B half
+  const int fr = lane & 15, fq = lane >> 4;        // fragment row / K chunk of this lane (MFMA layout)
 
   f32x4_t acc[2][2][TMQ][TNQ];
 #pragma unroll
@@ -312,104 +216,402 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
       for (int i = 0; i < TMQ; ++i)
 #pragma unroll
         for (int j = 0; j < TNQ; ++j) acc[a][b][i][j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-  bf16x8_t af[TMQ][2], bfr[TNQ][2];
 
-  auto read_a = [&](int buf, int h) {
-    const char* s = smem + buf * BUF + h * AH + a_row;
-#pragma unroll
-    for (int i = 0; i < TMQ; ++i) {
-      af[i][0] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw0);
-      af[i][1] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw1);
-    }
-  };
-  auto read_b = [&](int buf, int h) {
-    const char* s = smem + buf * BUF + 2 * AH + h * BH + b_row;
-#pragma unroll
-    for (int j = 0; j < TNQ; ++j) {
-      bfr[j][0] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw0);
-      bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw1);
-    }
-  };
-  auto mma = [&](f32x4_t (&c)[TMQ][TNQ]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < TMQ; ++i)
-#pragma unroll
-        for (int j = 0; j < TNQ; ++j)
-          c[i][j] = TR ? mfma16x16x32(bfr[j][s], af[i][s], c[i][j])
-                       : mfma16x16x32(af[i][s], bfr[j][s], c[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // prologue: K tile 0 fully staged and landed
-  prep_k(0);
-  stage_a(0, 0); stage_b(0, 0); stage_b(1, 0); stage_a(1, 0);
+  // the epilogue's bias and row-bias (temb) rows, loaded in the prologue beside the first DMA
   int rb_img0 = 0, rb_nimg = 0;
   if (p.rowbias) {
     rb_img0 = udiv22(tile_m, p.rb_div);
     rb_nimg = udiv22(min(p.M, tile_m + 256) - 1, p.rb_div) - rb_img0 + 1;
   }
   const bool rb_lds = rb_nimg <= RB_IMG;
-  for (int i = tid; i < BN_; i += 512) {
-    const int col = tile_n + i;
-    sbias[i] = (p.bias && col < p.N) ? p.bias[col] : 0.0f;
-  }
-  if (p.rowbias && rb_lds) {
-    for (int i = tid; i < rb_nimg * BN_; i += 512) {
-      const int im = i / BN_, c = i - im * BN_, col = tile_n + c;
-      srb[i] = col < p.N ? p.rowbias[(size_t)(rb_img0 + im) * p.ldrb + col] : 0.0f;
+  auto stage_bias = [&]() {
+    for (int i = tid; i < BN_; i += 512) {
+      const int col = tile_n + i;
+      sbias[i] = (p.bias && col < p.N) ? p.bias[col] : 0.0f;
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  BAR();
-  stamp(1);
-  if (late) BAR();
+    if (p.rowbias && rb_lds) {
+      for (int i = tid; i < rb_nimg * BN_; i += 512) {
+        const int im = i / BN_, c = i - im * BN_, col = tile_n + c;
+        srb[i] = col < p.N ? p.rowbias[(size_t)(rb_img0 + im) * p.ldrb + col] : 0.0f;
+      }
+    }
+  };
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1, nxt = cur ^ 1;
-    const bool more = kt + 1 < nk;
-    if (more) prep_k(kt + 1);
-    // phase 0: quadrant (0,0); stage A0(k+1)
-    read_a(cur, 0); read_b(cur, 0);
-    if (more) stage_a(0, nxt);
+  if constexpr (RING) {
+    // ---- Ring main loop. K is walked in 32-deep sub-tiles (256 A rows + BN_ B rows, 64 B each: SLOT bytes)
+    // through four LDS slots: in the segment that reads sub-tile s from slot s % 4, sub-tile s + 2 is
+    // LDS-DMA'd into slot (s + 2) % 4. One MFMA segment per sub-tile -- a wave's whole 4 TMQ TNQ fragment
+    // block (32 MFMAs at 256x256, 40 at 256x320) from 2 TMQ + 2 TNQ ds_read_b128 -- so two barriers per 32
+    // deep where the 4-phase loop below has four; that loop's MFMA pipe sat idle ~35 % of its main loop
+    // (SQ_VALU_MFMA_BUSY_CYCLES 62 % at 8192^3, in-kernel stamps 3170 cycles per 64-deep K tile against
+    // 2048 of MFMA issue), i.e. ~140 cycles per barrier.
+    // Stagger as in the 4-phase loop: waves 4-7 run one barrier behind, so each SIMD alternates one wave's
+    // read + DMA segment with the other's MFMA segment. Hazards (physical barrier k = k-th s_barrier; the
+    // early waves read sub-tile s in segment 2s + 1 and multiply it in 2s + 2, the late waves one segment
+    // later): slot (s + 2) % 4 last held sub-tile s - 2, whose late reads retired inside their MFMA segment
+    // 2s - 1, i.e. by barrier 2s, before any wave stages s + 2 (segment >= 2s + 1); sub-tile s + 1 is
+    // retired by every issuer before barrier 2s + 3 (early waves: after MFMA(s); late waves: after
+    // staging s + 2), the barrier its first reader (early, segment 2s + 3) passes.
+    constexpr int SLOT = (256 + BN_) * 64;
+    constexpr int NBP16 = BN_ / 16, NBJ16 = (NBP16 + 7) / 8;
+    static_assert(4 * SLOT == 2 * BUF, "the ring takes the 4-phase loop's LDS bytes");
+    // DMA wave-instructions a wave issues per sub-tile: 2 A pieces + its share of the B pieces (waves 0-3 take
+    // the odd ones: uniform per wave half, so each half's wait count is a constant)
+    constexpr int PW_E = 2 + (NBP16 + 7) / 8, PW_L = 2 + (NBP16 + 3) / 8;
+    // DMA piece = 16 rows x 64 B; lane -> row lane / 4 of the piece, physical 16-B chunk lane % 4 holding
+    // logical K chunk (lane % 4) ^ S[lane / 16], S = {0, 2, 3, 1} (= S[(row / 4) & 3]): a fragment read
+    // (row lane % 16, chunk lane / 16) then covers 16 distinct 16-B bank slots in every ds_read_b128 lane group
+    const int lrow = lane >> 2;
+    const int cch = (lane & 3) ^ ((0x78 >> (2 * (lane >> 4))) & 3);
+    RowPk rp[2];
+    unsigned aoff[2], aoff2[2], boff[NBJ16];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) rp[u] = pack_row<AMODE>(p, tile_m + (wave + 8 * u) * 16 + lrow);
+#pragma unroll
+    for (int u = 0; u < NBJ16; ++u) {
+      const int brow = tile_n + (wave + 8 * u) * 16 + lrow;
+      boff[u] = brow < p.N ? ((unsigned)brow * p.ldb + cch * 8) * 2u : OOB;
+    }
+    auto set_tap = [&](int tap) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int pix = tap_pixel8<AMODE>(p, rp[u], tap);
+        aoff[u] = pix < 0 ? OOB : ((unsigned)pix * p.lda + cch * 8) * 2u;
+        aoff2[u] = pix < 0 ? OOB : ((unsigned)pix * p.lda2 + cch * 8) * 2u;
+      }
+    };
+    set_tap(0);
+    const int ns = (p.K + 31) / 32, nfull = p.K / 32;
+    // staging state of the next sub-tile to stage, advanced by prep() in K order (tap-major conv K order:
+    // K index tap * Cin + c, the tap's pixel offsets re-derived when c wraps)
+    int s_tap = 0, s_c0 = 0, k_c0 = 0, k_k0 = 0;
+    bool k_second = false, k_tail = false;
+    auto prep = [&](int st) {
+      k_k0 = st * 32;
+      if (AMODE == 0) {
+        k_c0 = k_k0;
+      } else {
+        if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
+        k_c0 = s_c0;
+        s_c0 += 32;
+        if (s_c0 == cin) { s_c0 = 0; ++s_tap; }
+      }
+      k_second = two_src && k_c0 >= p.K1;
+      k_tail = st >= nfull;
+    };
+    // The K advance rides in the DMA's scalar offset (not range-checked; the per-lane voffset is, and carries
+    // OOB for rows outside the operand), so a piece costs no VALU: only the last sub-tile of a K that is not a
+    // multiple of 32 takes the per-lane tail test.
+    auto stage = [&](int slot) {
+      char* dst0 = smem + slot * SLOT;
+      const bool dead = k_tail && k_k0 + cch * 8 >= p.K;   // this lane's chunk lies past K (last sub-tile only)
+      const int soa = k_second ? (k_c0 - p.K1) * 2 : k_c0 * 2, sob = k_k0 * 2;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        unsigned off = k_second ? aoff2[u] : aoff[u];
+        if (dead) off = OOB;
+        lds_void* dst = (lds_void*)(dst0 + (wave + 8 * u) * 1024);
+        if (k_second) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra2, dst, 16, off, soa, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, off, soa, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < NBJ16; ++u) {
+        if (NBP16 % 8 == 0 || wave + 8 * u < NBP16) {
+          unsigned off = boff[u];
+          if (dead) off = OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + 256 * 64 + (wave + 8 * u) * 1024), 16, off,
+                                                   sob, 0, 0);
+        }
+      }
+    };
+    // fragment t of a 16-row block: row 16 t + lane % 16, logical chunk lane / 16 at its swizzled slot
+    const int frag = fr * 64 + ((fq ^ ((0x78 >> (2 * (fr >> 2))) & 3)) << 4);
+    const int a_base = (wr * TMQ * 16) * 64 + frag;
+    const int b_base = 256 * 64 + (wc * TNQ * 16) * 64 + frag;
+    bf16x8_t af[2][TMQ], bfr[2][TNQ];
+    auto read = [&](int slot) {
+      const char* s = smem + slot * SLOT;
+      auto ra_ = [&](int qm) {
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i)
+          af[qm][i] = *reinterpret_cast<const bf16x8_t*>(s + a_base + qm * 128 * 64 + i * 1024);
+      };
+      auto rb_ = [&](int qn) {
+#pragma unroll
+        for (int j = 0; j < TNQ; ++j)
+          bfr[qn][j] = *reinterpret_cast<const bf16x8_t*>(s + b_base + qn * (BN_ / 2) * 64 + j * 1024);
+      };
+      ra_(0); rb_(0); rb_(1); ra_(1);                  // in the order the quadrants below consume them
+    };
+    auto mma = [&]() {
+      constexpr int QM[4] = {0, 0, 1, 1}, QN[4] = {0, 1, 1, 0};
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < TMQ; ++i)
+#pragma unroll
+          for (int j = 0; j < TNQ; ++j) {
+            f32x4_t& c = acc[QM[q]][QN[q]][i][j];
+            c = TR ? mfma16x16x32(bfr[QN[q]][j], af[QM[q]][i], c) : mfma16x16x32(af[QM[q]][i], bfr[QN[q]][j], c);
+          }
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // retire sub-tile s + 1: everything but this wave's s + 2 pieces (when staged)
+    auto wait_next = [&](bool more, auto pw_c) {
+      if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(pw_c)::value) : "memory");
+    };
+
+    // prologue: sub-tiles 0 and 1 staged and landed
+    prep(0);
+    stage(0);
+    if (ns > 1) {
+      prep(1);
+      stage(1);
+    }
+    stage_bias();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     BAR();
-    mma(acc[0][0]);
-    // A1(k) is read in phase 2: retire it now (DMA'd in the previous tile's phase 3)
-    if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(1);
+    if (late) BAR();
+#if G8_RING_STAMPS
+    // diagnostic build only: per-wave cycle sums of the four segments of a ring iteration (read + DMA issue,
+    // first barrier, MFMA, second barrier), s_memtime with lgkmcnt(0) (so ds_read latency counts as read time)
+    unsigned long long sg[4] = {0, 0, 0, 0}, tprev = 0;
+    auto tick = [&]() {
+      unsigned long long t;
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      return t;
+    };
+    tprev = tick();
+#endif
+    for (int st = 0; st < ns; ++st) {
+      const bool more = st + 2 < ns;
+#if G8_RING_STAMPS
+      const unsigned long long t0 = tick();
+      if (st) sg[3] += t0 - tprev;
+#endif
+      if (!(p.tile & 0x8000)) read(st & 3);          // diagnostic 0x8000: no fragment reads (wrong output)
+      if (more && !(p.tile & 0x4000)) {                 // diagnostic 0x4000: no DMA in the loop (wrong output)
+        prep(st + 2);
+        stage((st + 2) & 3);
+      }
+      if (late) wait_next(more, std::integral_constant<int, PW_L>{});
+#if G8_RING_STAMPS
+      const unsigned long long t1 = tick();
+      sg[0] += t1 - t0;
+#endif
+      BAR();
+#if G8_RING_STAMPS
+      const unsigned long long t2 = tick();
+      sg[1] += t2 - t1;
+#endif
+      mma();
+      if (!late) wait_next(more, std::integral_constant<int, PW_E>{});
+#if G8_RING_STAMPS
+      tprev = tick();
+      sg[2] += tprev - t2;
+#endif
+      BAR();
+    }
+#if G8_RING_STAMPS
+    if (stamps && lane == 0 && stamp_wg < 512)
+      for (int k = 0; k < 4; ++k) g_gemm_stamps[(stamp_wg * 8 + wave) * 4 + k] = sg[k];
+#endif
+    if (!late) BAR();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     BAR();
-    // phase 1: quadrant (0,1); stage B0(k+1)
-    read_b(cur, 1);
-    if (more) stage_b(0, nxt);
+  } else {
+    // DMA: half-tile piece i (0..15) = rows [8i, 8i+8); wave w issues pieces w and w + 8.
+    // Lane -> (row 8i + lane/8, physical 16-B slot lane%8) holding logical K chunk slot ^ (row & 7).
+    const int lrow = lane >> 3;
+    const int cch = (lane & 7) ^ lrow;
+    // rows [h][u]: half h, piece w + 8u
+    RowPk rp[2][2];
+    unsigned aoff[2][2], aoff2[2][2], boff[2][NBJ];
+  #pragma unroll
+    for (int h = 0; h < 2; ++h) {
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        rp[h][u] = pack_row<AMODE>(p, tile_m + h * 128 + (wave + 8 * u) * 8 + lrow);
+      }
+  #pragma unroll
+      for (int u = 0; u < NBJ; ++u) {
+        const int brow = tile_n + h * (BN_ / 2) + (wave + 8 * u) * 8 + lrow;
+        boff[h][u] = brow < p.N ? ((unsigned)brow * p.ldb + cch * 8) * 2u : OOB;
+      }
+    }
+    auto set_tap = [&](int tap) {
+  #pragma unroll
+      for (int h = 0; h < 2; ++h)
+  #pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int pix = tap_pixel8<AMODE>(p, rp[h][u], tap);
+          aoff[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda + cch * 8) * 2u;
+          aoff2[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda2 + cch * 8) * 2u;
+        }
+    };
+    set_tap(0);
+    const int nk = (p.K + 63) / 64;
+    const int kfull = p.K / 64;
+
+    // per-K-tile staging parameters, advanced by prep_k() in K order
+    int s_tap = 0, s_c0 = 0, s_ky = 0, s_kx = 0;
+    int k_c0 = 0, k_k0 = 0, k_kb = 0;
+    bool k_second = false, k_tail = false;
+    const int ntap = AMODE == 0 ? 1 : p.K / cin;
+    auto prep_k = [&](int kt) {
+      k_k0 = kt * 64;
+      k_kb = k_k0;
+      if (AMODE == 0) {
+        k_c0 = k_k0;
+      } else if (AMODE == 1 && G8_CONV_CMAJOR == 2) {
+        // (ky, 64-channel slice, kx): the three kx taps of a slice -- the same image pixels shifted by one --
+        // are consecutive K tiles, so their re-reads meet in L2 one K tile apart instead of a channel pass apart
+        const int tap = s_ky * 3 + s_kx;
+        set_tap(tap);
+        k_c0 = s_c0;
+        k_kb = tap * cin + s_c0;
+        if (++s_kx == 3) {
+          s_kx = 0;
+          s_c0 += 64;
+          if (s_c0 == cin) { s_c0 = 0; ++s_ky; }
+        }
+      } else if (AMODE == 1 && G8_CONV_CMAJOR == 1) {
+        // 3x3 conv, 64-channel slice outer and tap inner: the nine taps of one slice read one ~4-image-row
+        // window of it in consecutive K tiles, so the window stays in L2 (tap-major order re-reads every
+        // input row from HBM once per tap row: 4.3 GB per level-0 conv dispatch for ~1.5 GB of operands).
+        // B's K offset follows (K index tap * Cin + c)
+        set_tap(s_tap);
+        k_c0 = s_c0;
+        k_kb = s_tap * cin + s_c0;
+        if (++s_tap == ntap) { s_tap = 0; s_c0 += 64; }
+      } else {
+        if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
+        k_c0 = s_c0;
+        s_c0 += 64;
+        if (s_c0 == cin) { s_c0 = 0; ++s_tap; }
+      }
+      k_second = two_src && k_c0 >= p.K1;
+      k_tail = kt >= kfull;
+    };
+    auto stage_a = [&](int h, int buf) {
+      char* dst0 = smem + buf * BUF + h * AH;
+  #pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        unsigned off = k_second ? aoff2[h][u] + (unsigned)(k_c0 - p.K1) * 2u : aoff[h][u] + (unsigned)k_c0 * 2u;
+        if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
+        lds_void* dst = (lds_void*)(dst0 + (wave + 8 * u) * 1024);
+        if (k_second) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra2, dst, 16, off, 0, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, off, 0, 0, 0);
+      }
+    };
+    auto stage_b = [&](int h, int buf) {
+      char* dst0 = smem + buf * BUF + 2 * AH + h * BH;
+  #pragma unroll
+      for (int u = 0; u < NBJ; ++u) {
+        if (NBP % 8 == 0 || wave + 8 * u < NBP) {
+          unsigned off = boff[h][u] + (unsigned)k_kb * 2u;
+          if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst0 + (wave + 8 * u) * 1024), 16, off, 0, 0, 0);
+        }
+      }
+    };
+
+    // fragment reads: row base + 16 t + lane%16, swizzle key row & 7 == lane & 7
+    const int fkey = lane & 7;
+    const int sw0 = ((0 + fq) ^ fkey) << 4, sw1 = ((4 + fq) ^ fkey) << 4;
+    const int a_row = (wr * TMQ * 16 + fr) * 128;   // inside an A half
+    const int b_row = (wc * TNQ * 16 + fr) * 128;   // inside a B half
+
+    bf16x8_t af[TMQ][2], bfr[TNQ][2];
+
+    auto read_a = [&](int buf, int h) {
+      const char* s = smem + buf * BUF + h * AH + a_row;
+  #pragma unroll
+      for (int i = 0; i < TMQ; ++i) {
+        af[i][0] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw0);
+        af[i][1] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw1);
+      }
+    };
+    auto read_b = [&](int buf, int h) {
+      const char* s = smem + buf * BUF + 2 * AH + h * BH + b_row;
+  #pragma unroll
+      for (int j = 0; j < TNQ; ++j) {
+        bfr[j][0] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw0);
+        bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw1);
+      }
+    };
+    auto mma = [&](f32x4_t (&c)[TMQ][TNQ]) {
+      __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int s = 0; s < 2; ++s)
+  #pragma unroll
+        for (int i = 0; i < TMQ; ++i)
+  #pragma unroll
+          for (int j = 0; j < TNQ; ++j)
+            c[i][j] = TR ? mfma16x16x32(bfr[j][s], af[i][s], c[i][j])
+                         : mfma16x16x32(af[i][s], bfr[j][s], c[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+
+    // prologue: K tile 0 fully staged and landed
+    prep_k(0);
+    stage_a(0, 0); stage_b(0, 0); stage_b(1, 0); stage_a(1, 0);
+    stage_bias();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     BAR();
-    mma(acc[0][1]);
+    stamp(1);
+    if (late) BAR();
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1, nxt = cur ^ 1;
+      const bool more = kt + 1 < nk;
+      if (more) prep_k(kt + 1);
+      // phase 0: quadrant (0,0); stage A0(k+1)
+      read_a(cur, 0); read_b(cur, 0);
+      if (more) stage_a(0, nxt);
+      BAR();
+      mma(acc[0][0]);
+      // A1(k) is read in phase 2: retire it now (DMA'd in the previous tile's phase 3)
+      if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      BAR();
+      // phase 1: quadrant (0,1); stage B0(k+1)
+      read_b(cur, 1);
+      if (more) stage_b(0, nxt);
+      BAR();
+      mma(acc[0][1]);
+      BAR();
+      // phase 2: quadrant (1,1); stage B1(k+1)
+      read_a(cur, 1);
+      if (more) stage_b(1, nxt);
+      BAR();
+      mma(acc[1][1]);
+      // A0(k+1), B0(k+1) are read in the next tile's phase 0: retire everything but this wave's B1(k+1)
+      // pieces (nbw: 3 / 2 for the 256x320 tile's two wave halves, 2 at 256x256, 1 at 256x128)
+      if (nbw >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (nbw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (nbw == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      BAR();
+      // phase 3: quadrant (1,0); stage A1(k+1)
+      read_b(cur, 0);
+      if (more) stage_a(1, nxt);
+      BAR();
+      mma(acc[1][0]);
+      // B1(k+1) is read in the next tile's phase 1
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      BAR();
+    }
+    if (!late) BAR();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     BAR();
-    // phase 2: quadrant (1,1); stage B1(k+1)
-    read_a(cur, 1);
-    if (more) stage_b(1, nxt);
-    BAR();
-    mma(acc[1][1]);
-    // A0(k+1), B0(k+1) are read in the next tile's phase 0: retire everything but this wave's B1(k+1)
-    // pieces (nbw: 3 / 2 for the 256x320 tile's two wave halves, 2 at 256x256, 1 at 256x128)
-    if (nbw >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if (nbw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if (nbw == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    BAR();
-    // phase 3: quadrant (1,0); stage A1(k+1)
-    read_b(cur, 0);
-    if (more) stage_a(1, nxt);
-    BAR();
-    mma(acc[1][0]);
-    // B1(k+1) is read in the next tile's phase 1
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    BAR();
+
   }
-  if (!late) BAR();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  BAR();
   stamp(2);
 
   if (p.tile & 0x100) {                          // diagnostic: main loop only (keeps acc live)
@@ -802,31 +1004,50 @@ extern "C" int acth_debug_gemm_stamps(unsigned long long* host_dst, int n_wgs) {
   return ACTH_OK;
 }
 
-template <int BN_>
-static void launch8p(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
-                     int vec_ok, hipStream_t stream) {
+template <int BN_, bool RING>
+static void launch8p_(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
+                      int vec_ok, hipStream_t stream) {
   if constexpr (BN_ == 256) {
     if (d->act == 2 && d->amode == 0) {     // GEGLU: gated outputs straight from the transposed accumulators
-      hipLaunchKernelGGL((gemm8p_kernel<256, 0, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes,
-                         vec_ok);
+      hipLaunchKernelGGL((gemm8p_kernel<256, 0, true, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                         b_bytes, vec_ok);
       return;
     }
   }
-  if (G8_TR_ALL == 1 || (G8_TR_ALL == 2 && !d->R && !d->MIX)) {
-    if (d->amode == 1)
-      hipLaunchKernelGGL((gemm8p_kernel<BN_, 1, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
-    else if (d->amode == 2)
-      hipLaunchKernelGGL((gemm8p_kernel<BN_, 2, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
-    else
-      hipLaunchKernelGGL((gemm8p_kernel<BN_, 0, true>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
-    return;
+  if constexpr (G8_TR_ALL != 0) {
+    if (G8_TR_ALL == 1 || (!d->R && !d->MIX)) {
+      if (d->amode == 1)
+        hipLaunchKernelGGL((gemm8p_kernel<BN_, 1, true, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                           b_bytes, vec_ok);
+      else if (d->amode == 2)
+        hipLaunchKernelGGL((gemm8p_kernel<BN_, 2, true, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                           b_bytes, vec_ok);
+      else
+        hipLaunchKernelGGL((gemm8p_kernel<BN_, 0, true, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                           b_bytes, vec_ok);
+      return;
+    }
   }
   if (d->amode == 1)
-    hipLaunchKernelGGL((gemm8p_kernel<BN_, 1>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+    hipLaunchKernelGGL((gemm8p_kernel<BN_, 1, false, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                       b_bytes, vec_ok);
   else if (d->amode == 2)
-    hipLaunchKernelGGL((gemm8p_kernel<BN_, 2>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+    hipLaunchKernelGGL((gemm8p_kernel<BN_, 2, false, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                       b_bytes, vec_ok);
   else
-    hipLaunchKernelGGL((gemm8p_kernel<BN_, 0>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes, b_bytes, vec_ok);
+    hipLaunchKernelGGL((gemm8p_kernel<BN_, 0, false, RING>), grid, dim3(512), 0, stream, *d, a_bytes, a2_bytes,
+                       b_bytes, vec_ok);
+}
+
+// Main-loop choice: the ring for the 3x3 convs (+6-11 % on the UNet conv shapes, tools/ab_gemm.py,
+// profiles/r6_ring_ab.log), the 4-phase loop elsewhere (dense shapes within -6..+8 %, the small-K projections
+// slower on the ring). Tile bit 0x1000 forces the ring, 0x2000 the 4-phase loop (A/B in one process).
+template <int BN_>
+static void launch8p(const ActhGemmDesc* d, dim3 grid, unsigned a_bytes, unsigned a2_bytes, unsigned b_bytes,
+                     int vec_ok, hipStream_t stream) {
+  const bool ring = (d->tile & 0x1000) || (!(d->tile & 0x2000) && d->amode == 1);
+  if (ring) launch8p_<BN_, true>(d, grid, a_bytes, a2_bytes, b_bytes, vec_ok, stream);
+  else launch8p_<BN_, false>(d, grid, a_bytes, a2_bytes, b_bytes, vec_ok, stream);
 }
 
 // Row-block group of the M-grouped raster: explicit in tile bits 16-23 (bench / tests), else

@@ -339,6 +339,42 @@ def test_gemm_tile_variants(dev, tile):
         assert rel(out, h * F.gelu(g)) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [4, 5, 6, 7])
+def test_gemm_ring_matches_phased(dev, tile):
+    """The phased kernels' ring main loop (tile bit 0x1000) against their 4-phase loop (0x2000): both add the
+    K chunks to every accumulator in the same order, so the outputs are bitwise equal -- dense with a ragged K
+    tail (K % 32 = 8), two-source concat, conv3x3 stride 1 / 2 / upsample with a skip concat, temporal (3,1,1)
+    and GEGLU."""
+    from actalker_amd.modules import pack_conv3x3, pack_conv3d_t, pack_geglu
+
+    def both(*args, **kw):
+        return ops.gemm(*args, tile=tile | 0x1000, **kw), ops.gemm(*args, tile=tile | 0x2000, **kw)
+
+    M, N, K = 1100, 330, 200
+    a, w = bf(rnd(M, K)), bf(rnd(N, K, scale=K ** -0.5))
+    r, o = both(a.to(dev), w.to(dev), bias=rnd(N).to(dev), residual=bf(rnd(M, N)).to(dev))
+    assert torch.equal(r, o)
+    a1, a2, w2 = bf(rnd(M, 192)), bf(rnd(M, 128)), bf(rnd(N, 320, scale=320 ** -0.5))
+    r, o = both(a1.to(dev), w2.to(dev), a2=a2.to(dev), rowbias=rnd(4, N).to(dev), rb_div=300)
+    assert torch.equal(r, o)
+    B, H, W, C1, C2, Co = 2, 12, 20, 128, 64, 320
+    tok = lambda t_: t_.permute(0, 2, 3, 1).reshape(-1, t_.shape[1]).contiguous().to(dev)
+    x1, x2 = tok(bf(rnd(B, C1, H, W))), tok(bf(rnd(B, C2, H, W)))
+    wc = pack_conv3x3(bf(rnd(Co, C1 + C2, 3, 3, scale=(9 * (C1 + C2)) ** -0.5))).to(dev)
+    for st, up in ((1, False), (2, False), (1, True)):
+        Ho, Wo = (2 * H, 2 * W) if up else ((H - 1) // st + 1, (W - 1) // st + 1)
+        r, o = both(x1, wc, a2=x2, conv=dict(H=H, W=W, Ho=Ho, Wo=Wo, stride=st, upsample=up, B=B))
+        assert torch.equal(r, o), (st, up)
+    x = bf(rnd(2 * 7 * 40, 128))
+    wt = pack_conv3d_t(bf(rnd(160, 128, 3, 1, 1, scale=384 ** -0.5))).to(dev)
+    r, o = both(x.to(dev), wt, temporal=dict(F=7, S=40))
+    assert torch.equal(r, o)
+    if tile == 4:
+        wp, bp = pack_geglu(rnd(1280, 192, scale=192 ** -0.5), rnd(1280, scale=0.1))
+        r, o = both(bf(rnd(600, 192)).to(dev), wp.to(dev), bias=bp.to(dev), act=ops.ACT_GEGLU)
+        assert torch.equal(r, o)
+
+
 def test_gemm_tall_skinny_auto_tile(dev):
     """The Mamba x_proj shape class (N = 2 (R + 32) <= 128 over >= 65536 rows, fp32 out) auto-selects
     the phased 256x128 kernel; ragged last row tile, N not a multiple of 16."""

@@ -15,6 +15,22 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ACTH_LIB") or os.path.join(_HERE, "libactalker_hip.so")
 LIB_PATH_F16 = os.environ.get("ACTH_LIB_F16") or os.path.join(_HERE, "libactalker_hip_f16.so")
 
+def kernel_source_digest() -> str:
+    """SHA-256 (16 hex digits) of the HIP kernel sources and the C ABI header: identifies the kernels a measured
+    figure belongs to (PMC traffic files record it; bench.py drops figures recorded for other sources)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.h")))
+    files.append(os.path.join(os.path.dirname(_HERE), "include", "actalker_hip.h"))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+
 c_int = ctypes.c_int
 c_float = ctypes.c_float
 c_ll = ctypes.c_longlong

@@ -686,7 +686,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 }
 
 extern "C" int acth_flash_attn(const ActhAttnDesc* d, hipStream_t stream) {
-  if (d && (d->nbatch == 0 || d->nheads == 0 || d->Sq == 0)) return ACTH_OK;   // no work: nothing read
+  // no work (the other sizes in range): nothing read
+  if (d && d->nbatch >= 0 && d->nheads >= 0 && d->Sq >= 0 && d->Skv >= 0 &&
+      (d->nbatch == 0 || d->nheads == 0 || d->Sq == 0))
+    return ACTH_OK;
   if (!d || !d->q || !d->k || !d->v || !d->o) return ACTH_EINVAL;
   if (d->Sq <= 0 || d->Skv <= 0 || d->nheads <= 0 || d->nbatch <= 0) return ACTH_EINVAL;
   if (d->ldq % 8 || d->ldk % 8 || d->ldv % 8 || d->ldo % 4) return ACTH_EINVAL;
@@ -859,7 +862,9 @@ __global__ __launch_bounds__(256) void temporal_attn_mfma_kernel(const ActhTempo
 }
 
 extern "C" int acth_temporal_attn(const ActhTemporalAttnDesc* d, hipStream_t stream) {
-  if (d && (d->B == 0 || d->S == 0 || d->H == 0)) return ACTH_OK;   // no work: nothing read
+  // no work (the other sizes in range): nothing read
+  if (d && d->B >= 0 && d->S >= 0 && d->H >= 0 && d->F > 0 && d->F <= 32 && (d->B == 0 || d->S == 0 || d->H == 0))
+    return ACTH_OK;
   if (!d || !d->qkv || !d->o) return ACTH_EINVAL;
   if (d->F <= 0 || d->F > 32 || d->B <= 0 || d->S <= 0 || d->H <= 0) return ACTH_EINVAL;
   if (d->ldqkv % 8 || d->ldo % 8) return ACTH_EINVAL;
@@ -959,7 +964,8 @@ __global__ __launch_bounds__(256) void ip_attn_kernel(const ActhIpAttnDesc p) {
 }
 
 extern "C" int acth_ip_attn(const ActhIpAttnDesc* d, hipStream_t stream) {
-  if (d && d->M == 0) return ACTH_OK;   // no work: nothing read
+  // no work (the other sizes in range): nothing read
+  if (d && d->M == 0 && d->H >= 0 && d->S >= 0 && d->rows_per_ctx >= 0) return ACTH_OK;
   if (!d || !d->vbase || !d->out) return ACTH_EINVAL;
   if (d->kv && (!d->q || d->nkeys <= 0 || d->nkeys > 32 || d->ldkv % 8 || d->ldq % 8)) return ACTH_EINVAL;
   if (d->M <= 0 || d->H <= 0 || d->rows_per_ctx <= 0 || d->S <= 0) return ACTH_EINVAL;

@@ -23,15 +23,10 @@
 
 using namespace gemm;
 
-// 1: 3x3-conv K order with the 64-channel slice outer and the tap inner (L2 reuse of the nine taps'
-// shared window). Measured slower in isolation (level-0 conv 951 -> 881 TFLOP/s, level 2 1106 -> 945,
-// profiles/r3_step31_conv_order_rejected.log), so off. 2: (ky, slice, kx), the three kx taps of a slice in
-// consecutive K tiles: 11-20 % slower on every conv shape (level 0 985 -> 875, level 1 1066 -> 910, level 2
-// 1133 -> 940; profiles/r5_conv_korder_rejected.log) -- re-deriving the four rows' tap offsets every K tile
-// costs more than the L2 reuse returns
-#ifndef G8_CONV_CMAJOR
-#define G8_CONV_CMAJOR 0
-#endif
+// 3x3-conv K order: tap-major (K index tap * Cin + c). Two L2-reuse orders were measured and dropped: the
+// 64-channel slice outer / tap inner (level-0 conv 951 -> 881 TFLOP/s, profiles/r3_step31_conv_order_rejected.log)
+// and (ky, slice, kx) (11-20 % slower on every conv shape, profiles/r5_conv_korder_rejected.log): re-deriving
+// the rows' tap offsets every K tile costs more than the L2 reuse returns.
 // 1: 3x3-conv rows (no upsample) carry their tap-(0, 0) pixel and a 9-bit in-image tap mask
 #ifndef G8_RING_STAMPS
 #define G8_RING_STAMPS 0      // 1: diagnostic build, per-wave segment cycle sums of the ring loop (tile bit 0x400)
@@ -432,22 +427,22 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     // rows [h][u]: half h, piece w + 8u
     RowPk rp[2][2];
     unsigned aoff[2][2], aoff2[2][2], boff[2][NBJ];
-  #pragma unroll
+#pragma unroll
     for (int h = 0; h < 2; ++h) {
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < 2; ++u) {
         rp[h][u] = pack_row<AMODE>(p, tile_m + h * 128 + (wave + 8 * u) * 8 + lrow);
       }
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < NBJ; ++u) {
         const int brow = tile_n + h * (BN_ / 2) + (wave + 8 * u) * 8 + lrow;
         boff[h][u] = brow < p.N ? ((unsigned)brow * p.ldb + cch * 8) * 2u : OOB;
       }
     }
     auto set_tap = [&](int tap) {
-  #pragma unroll
+#pragma unroll
       for (int h = 0; h < 2; ++h)
-  #pragma unroll
+#pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int pix = tap_pixel8<AMODE>(p, rp[h][u], tap);
           aoff[h][u] = pix < 0 ? OOB : ((unsigned)pix * p.lda + cch * 8) * 2u;
@@ -459,36 +454,14 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     const int kfull = p.K / 64;
 
     // per-K-tile staging parameters, advanced by prep_k() in K order
-    int s_tap = 0, s_c0 = 0, s_ky = 0, s_kx = 0;
+    int s_tap = 0, s_c0 = 0;
     int k_c0 = 0, k_k0 = 0, k_kb = 0;
     bool k_second = false, k_tail = false;
-    const int ntap = AMODE == 0 ? 1 : p.K / cin;
     auto prep_k = [&](int kt) {
       k_k0 = kt * 64;
       k_kb = k_k0;
       if (AMODE == 0) {
         k_c0 = k_k0;
-      } else if (AMODE == 1 && G8_CONV_CMAJOR == 2) {
-        // (ky, 64-channel slice, kx): the three kx taps of a slice -- the same image pixels shifted by one --
-        // are consecutive K tiles, so their re-reads meet in L2 one K tile apart instead of a channel pass apart
-        const int tap = s_ky * 3 + s_kx;
-        set_tap(tap);
-        k_c0 = s_c0;
-        k_kb = tap * cin + s_c0;
-        if (++s_kx == 3) {
-          s_kx = 0;
-          s_c0 += 64;
-          if (s_c0 == cin) { s_c0 = 0; ++s_ky; }
-        }
-      } else if (AMODE == 1 && G8_CONV_CMAJOR == 1) {
-        // 3x3 conv, 64-channel slice outer and tap inner: the nine taps of one slice read one ~4-image-row
-        // window of it in consecutive K tiles, so the window stays in L2 (tap-major order re-reads every
-        // input row from HBM once per tap row: 4.3 GB per level-0 conv dispatch for ~1.5 GB of operands).
-        // B's K offset follows (K index tap * Cin + c)
-        set_tap(s_tap);
-        k_c0 = s_c0;
-        k_kb = s_tap * cin + s_c0;
-        if (++s_tap == ntap) { s_tap = 0; s_c0 += 64; }
       } else {
         if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
         k_c0 = s_c0;
@@ -500,7 +473,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     };
     auto stage_a = [&](int h, int buf) {
       char* dst0 = smem + buf * BUF + h * AH;
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < 2; ++u) {
         unsigned off = k_second ? aoff2[h][u] + (unsigned)(k_c0 - p.K1) * 2u : aoff[h][u] + (unsigned)k_c0 * 2u;
         if (k_tail && k_k0 + cch * 8 >= p.K) off = OOB;
@@ -511,7 +484,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     };
     auto stage_b = [&](int h, int buf) {
       char* dst0 = smem + buf * BUF + 2 * AH + h * BH;
-  #pragma unroll
+#pragma unroll
       for (int u = 0; u < NBJ; ++u) {
         if (NBP % 8 == 0 || wave + 8 * u < NBP) {
           unsigned off = boff[h][u] + (unsigned)k_kb * 2u;
@@ -531,7 +504,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
 
     auto read_a = [&](int buf, int h) {
       const char* s = smem + buf * BUF + h * AH + a_row;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < TMQ; ++i) {
         af[i][0] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw0);
         af[i][1] = *reinterpret_cast<const bf16x8_t*>(s + i * 2048 + sw1);
@@ -539,7 +512,7 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     };
     auto read_b = [&](int buf, int h) {
       const char* s = smem + buf * BUF + 2 * AH + h * BH + b_row;
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < TNQ; ++j) {
         bfr[j][0] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw0);
         bfr[j][1] = *reinterpret_cast<const bf16x8_t*>(s + j * 2048 + sw1);
@@ -547,11 +520,11 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     };
     auto mma = [&](f32x4_t (&c)[TMQ][TNQ]) {
       __builtin_amdgcn_s_setprio(1);
-  #pragma unroll
+#pragma unroll
       for (int s = 0; s < 2; ++s)
-  #pragma unroll
+#pragma unroll
         for (int i = 0; i < TMQ; ++i)
-  #pragma unroll
+#pragma unroll
           for (int j = 0; j < TNQ; ++j)
             c[i][j] = TR ? mfma16x16x32(bfr[j][s], af[i][s], c[i][j])
                          : mfma16x16x32(af[i][s], bfr[j][s], c[i][j]);

@@ -21,7 +21,9 @@
  *     when the launch failed;
  *   - a call with no work (zero rows / an empty batch: M, B, nbatch, nb, Sq = 0, as torch ops accept empty
  *     tensors) returns ACTH_OK without launching and reads no pointer (an empty tensor's data pointer may
- *     be NULL); negative sizes stay ACTH_EINVAL.
+ *     be NULL). A negative value of that primary size stays ACTH_EINVAL; the attention entry points also
+ *     check their other sizes (>= 0, F in 1..32) before the no-work return, the others do not inspect
+ *     the remaining fields of a call with no work.
  */
 #ifndef ACTALKER_HIP_H
 #define ACTALKER_HIP_H

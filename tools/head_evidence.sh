@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 if [ "$PART" = A ]; then
   bash tools/pmc_pass.sh "$OUT/pmc" || exit $?
   python tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc_traffic.csv" || exit $?
-  python tools/pmc_summary.py "$OUT/pmc" --json profiles/pmc_traffic.json --workload "mode0 576x1024 f14 fpb14 bf16" \
+  python tools/pmc_summary.py "$OUT/pmc" --json profiles/pmc_traffic.json --workload "$(cat "$OUT/pmc/workload.txt")" \
       --source "profiles/${ROUND}_pmc_traffic.csv (tools/pmc_pass.sh: bench.py --steps 1 --warmup 0, mode 0 default config, FETCH_SIZE and WRITE_SIZE passes, $ROUND HEAD $SHA)" || exit $?
   cp profiles/pmc_traffic.json "$OUT/pmc_traffic.json"
   bash tools/gpu_check.sh "$TAG"

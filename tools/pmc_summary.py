@@ -44,7 +44,10 @@ def main():
                 "layernorm": lambda k: "layernorm" in k, "geglu_ffn": lambda k: "ffn_geglu" in k,
                 "mamba_combine": lambda k: "mamba_combine" in k}
         # the bench configuration the counted run used (bench.py only reports traffic for that same workload)
-        res = {"_workload": sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None}
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from actalker_amd._lib import kernel_source_digest
+        res = {"_workload": sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else None,
+               "_kernel_sources": kernel_source_digest()}
         for fam, match in fams.items():
             g = [r for r in rows if match(r[0].split("(")[0].replace("void ", ""))]
             n = sum(r[1] for r in g)

@@ -425,7 +425,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
                        cross_attention_kwargs: Optional[Dict[str, Any]] = None,
                        spatial_condition_rmap: Optional[torch.Tensor] = None, out_f32: bool = True,
                        spatial_condition_rmap_max: Optional[int] = None,
-                       prefix_src: Optional[Sequence[int]] = None):
+                       prefix_src: Optional[Sequence[int]] = None, out: Optional[torch.Tensor] = None):
         """Token-major entry: x_tok (B*F*H*W, in_channels) -> (B*F*H*W, out_channels), computed with
         ``compute_dtype()`` activations (token inputs in another dtype are converted on entry).
         ``spatial_condition_rmap`` (device int32, one entry per frame) remaps frame rows of
@@ -437,7 +437,9 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         does. The caller guarantees those elements' latent rows, spatial condition rows, timestep and
         added time ids are equal (the pipeline's CFG branches 1-3 of one window differ only in the audio /
         VASA / ID prompts, pipeline:162-200); the prefix then runs once per distinct element and its
-        rows are copied out (exact: every op there is per batch element)."""
+        rows are copied out (exact: every op there is per batch element).
+
+        ``out`` (optional, (B*F*H*W, out_channels) rows of the output dtype): conv_out writes there directly."""
         if self.device.type != "cuda":
             raise RuntimeError("UNetSpatioTemporalConditionModel (actalker_amd) runs on the MI355X HIP kernels "
                                "only; move it to a GPU device first")
@@ -449,11 +451,11 @@ class UNetSpatioTemporalConditionModel(nn.Module):
                 spatial_condition_tok = spatial_condition_tok.to(dt)
             return self._forward_tokens(x_tok, B, F, H, W, timestep, encoder_hidden_states, added_time_ids,
                                         spatial_condition_tok, cross_attention_kwargs, spatial_condition_rmap,
-                                        out_f32, spatial_condition_rmap_max, prefix_src)
+                                        out_f32, spatial_condition_rmap_max, prefix_src, out)
 
     def _forward_tokens(self, x_tok, B, F, H, W, timestep, encoder_hidden_states, added_time_ids,
                         spatial_condition_tok, cross_attention_kwargs, spatial_condition_rmap, out_f32,
-                        spatial_condition_rmap_max, prefix_src):
+                        spatial_condition_rmap_max, prefix_src, out=None):
         ctx = self._prep_ctx(B, F, timestep, encoder_hidden_states, added_time_ids, cross_attention_kwargs)
         S0 = H * W
         uniq = None
@@ -524,7 +526,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             h, H, W = blk.run(ctx, h, skips, H, W)
         g, b = self.conv_norm_out.gb()
         n = ops.groupnorm(h, g, b, self.conv_norm_out.eps, H * W, silu=True)
-        return ops.conv3x3(n, self.conv_out.w3(), BF, H, W, bias=self.conv_out.b(), out_f32=out_f32)
+        return ops.conv3x3(n, self.conv_out.w3(), BF, H, W, bias=self.conv_out.b(), out_f32=out_f32, out=out)
 
     def _prefix_capable(self) -> bool:
         from .modules import CrossAttnDownBlockSpatioTemporal

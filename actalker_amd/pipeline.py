@@ -261,6 +261,13 @@ class HipBackend:
             self._frame_eq = eq
         return self._frame_eq
 
+    def begin_schedule(self, timesteps: Sequence[float]):
+        """The sampler's timesteps, uploaded once per denoise() call (one host -> device copy) and handed out to the
+        UNet calls as device scalars."""
+        vals = [float(v) for v in timesteps]
+        dev_t = torch.tensor(vals, dtype=torch.float32).to(self.dev)
+        self._t_table = {v: dev_t[k:k + 1] for k, v in enumerate(vals)}
+
     def begin_step(self, raw_frames: List[List[int]]):
         self._raw = raw_frames
 
@@ -289,8 +296,8 @@ class HipBackend:
         fl_h = [f for (w, _c) in units for f in frames[w]]
         fidx_d = self._dev_ints(fl_h, torch.int32)
         br_d = self._dev_ints([c for (_w, c) in units], torch.int64)
-        x = ops.window_input(lat, fidx_d, self.img, br_d.to(torch.int32), 1.0 / math.sqrt(sigma * sigma + 1.0),
-                             U, F, S, self.T)
+        br32_d = self._dev_ints([c for (_w, c) in units], torch.int32)
+        x = ops.window_input(lat, fidx_d, self.img, br32_d, 1.0 / math.sqrt(sigma * sigma + 1.0), U, F, S, self.T)
         # the units' conditioning rows (ID / audio / VASA prompts, added time ids): fixed for the whole sampling
         # run, and the loop's (frames, branches) layouts repeat (the window shift cycles), so each layout is
         # gathered once and reused -- no index kernels inside the steady-state step
@@ -304,7 +311,11 @@ class HipBackend:
         ide_r, aud_r, vas_r, added_r = got
         ehs = (ide_r, [aud_r, vas_r])
         cak = {"ip_adapter_masks": self.masks, "acth_gate": self.gate}
-        tt = torch.full((1,), t, device=self.dev, dtype=torch.float32)
+        # the step's timestep as a device scalar: a view into the schedule's table (begin_schedule) when the loop
+        # announced it -- no fill kernel per call
+        tt = self._t_table.get(t) if getattr(self, "_t_table", None) else None
+        if tt is None:
+            tt = torch.full((1,), t, device=self.dev, dtype=torch.float32)
         prmap, pmax = fidx_d, max(fl_h)
         if self.pose_P != self.T:
             pr = [r % self.pose_P for (w, _c) in units for r in self._raw[w]]
@@ -428,6 +439,8 @@ def denoise(backend, latents_all: torch.Tensor, cfg: LoopConfig, rank: int = 0, 
         frame_eq = flags.cpu().bool()
     if hasattr(backend, "share_prefix"):
         backend.share_prefix = cfg.share_cfg_prefix
+    if hasattr(backend, "begin_schedule"):
+        backend.begin_schedule(timesteps)
     S = backend.S
     rows_per_unit = F * S
     cap_max = math.ceil(n_windows * 4 / world)

@@ -361,6 +361,17 @@ class FamilyTimer:
                     state_updates_per_launch=round(upd), v_exp_per_s=V_EXP_PER_S, floor_us=round(floor_us, 1),
                     frac=round(floor_us / (1000.0 * ms / len(evs)), 4),
                     source="profiles/r3_step18_valu_probe.txt (v_exp_f32, 4 waves / SIMD)")
+                # the kernel's whole VALU issue, not only its exponentials: per token a lane updates 8 states with
+                # 8 v_exp_f32, 8 v_pk_mul_f32, 8 v_pk_fma_f32 and ~12 single-rate VALU (u / y conversion, pair
+                # reduction, D skip; the ISA of scan_pair_kernel<20,128,1,1>), priced at the probe's chip-wide
+                # throughput per wave-instruction at 4 waves / SIMD
+                per_512 = 8 * VALU_S["v_exp_f32"] + 8 * VALU_S["v_pk_mul_f32"] + 8 * VALU_S["v_pk_fma_f32"] + \
+                    12 * VALU_S["v_fma_f32"]
+                vfloor_us = upd / 512.0 * per_512 * 1e6
+                out[fam]["valu_floor"] = dict(
+                    floor_us=round(vfloor_us, 1), frac=round(vfloor_us / (1000.0 * ms / len(evs)), 4),
+                    instructions_per_lane_token="8 v_exp + 8 v_pk_mul + 8 v_pk_fma + 12 VALU (8 states)",
+                    source="profiles/r3_step18_valu_probe.txt (chip-wide time per wave-instruction, 4 waves / SIMD)")
             pmc = pmc_traffic(fam)
             if pmc:
                 # PMC bytes per kernel dispatch x dispatches per op call (GroupNorm: stats + apply)
@@ -372,6 +383,9 @@ class FamilyTimer:
 
 
 V_EXP_PER_S = 4096 * 16384 * 64 / 0.239e-3      # gfx950 v_exp_f32 issue rate, all 1024 SIMDs (valu_probe)
+# chip-wide seconds per wave-instruction at 4 waves / SIMD (valu_probe: 4096 waves x 16384 instructions)
+VALU_S = {k: ms * 1e-3 / (4096 * 16384) for k, ms in
+          (("v_exp_f32", 0.239), ("v_pk_mul_f32", 0.150), ("v_pk_fma_f32", 0.167), ("v_fma_f32", 0.089))}
 
 
 def cpu_baseline(unet, H, W, frames=2, mode=0):

@@ -279,23 +279,15 @@ __global__ __launch_bounds__(512, 2) void gemm8p_kernel(const ActhGemmDesc p, un
     const int ns = (p.K + 31) / 32, nfull = p.K / 32;
     // staging state of the next sub-tile to stage, advanced by prep() in K order (tap-major conv K order:
     // K index tap * Cin + c, the tap's pixel offsets re-derived when c wraps)
+    // (tap-major conv K order; the 32-channel-slice-outer order, whose nine taps of a slice read one ~4-row window in
+    // consecutive sub-tiles, measured 6-16 % slower on every conv shape on the ring too: profiles/r6_cslice_ab.log)
     int s_tap = 0, s_c0 = 0, k_c0 = 0, k_k0 = 0, k_kb = 0;
     bool k_second = false, k_tail = false;
-    // tile bit 0x200 (3x3 convs): 32-channel slice outer, tap inner -- the nine taps of a slice read one
-    // ~4-image-row window of it in consecutive sub-tiles (~32 KB per tile, ~1 MB for an XCD's resident tiles,
-    // against the whole K loop's ~10 MB in tap-major order); B's K index follows (tap * Cin + c)
-    const bool cslice = AMODE == 1 && (p.tile & 0x200);
-    const int ntap = AMODE == 1 ? 9 : 1;
     auto prep = [&](int st) {
       k_k0 = st * 32;
       k_kb = k_k0;
       if (AMODE == 0) {
         k_c0 = k_k0;
-      } else if (cslice) {
-        set_tap(s_tap);
-        k_c0 = s_c0;
-        k_kb = s_tap * cin + s_c0;
-        if (++s_tap == ntap) { s_tap = 0; s_c0 += 32; }
       } else {
         if (s_c0 == 0 && s_tap > 0) set_tap(s_tap);
         k_c0 = s_c0;

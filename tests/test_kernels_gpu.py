@@ -366,9 +366,6 @@ def test_gemm_ring_matches_phased(dev, tile):
         cv = dict(H=H, W=W, Ho=Ho, Wo=Wo, stride=st, upsample=up, B=B)
         r, o = both(x1, wc, a2=x2, conv=cv)
         assert torch.equal(r, o), (st, up)
-        # slice-outer K order (tile bit 0x200): same products, another summation order -- fp32-close
-        s_ = ops.gemm(x1, wc, a2=x2, conv=cv, tile=tile | 0x1000 | 0x200)
-        assert rel(s_, r) < 2e-3, (st, up)
     x = bf(rnd(2 * 7 * 40, 128))
     wt = pack_conv3d_t(bf(rnd(160, 128, 3, 1, 1, scale=384 ** -0.5))).to(dev)
     r, o = both(x.to(dev), wt, temporal=dict(F=7, S=40))

@@ -374,7 +374,9 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
     call evaluates branches 0, 1, 3, against ``win14_mode1`` (the reference run for those three). ``frames`` 25: the
     reference's shipped window (config/inference.yaml:4 n_sample_frames) at 576x1024, mode 0, against ``win25_mode0``:
     the temporal attention's two-block (F <= 32) kernel at the real widths. ``w_px`` 576: BASELINE C1's geometry
-    (576x576), mode 0, against ``c1win14_mode0`` (floor: the 576x1024 mode-0 one).
+    (576x576), mode 0, against ``c1win14_mode0``, each unit held to 1.5x C1's own rounding floor for that unit
+    (tests/golden/unet_c1win14_mode0_floor.safetensors: bf16 1.72-1.80e-2, fp16 2.2e-3 -- the 576x576 call loses
+    more to bf16 rounding than the 576x1024 one's 1.40e-2), capped at 2e-2.
     Stated tolerance per unit: 1.5x the bf16 (fp16) rounding floor the oracle shows at this geometry and weights
     (tests/golden/unet_full_mode0_rounded.safetensors for mode 0, unet_full_half_rounded.safetensors -- the same
     [lower, upper] mask split with both prompts live -- for mode 2: every op's inputs / outputs rounded at its
@@ -398,6 +400,14 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
     floor = load_file(os.path.join(GOLD, f"unet_full_{fcase}_rounded.safetensors"))
     full = load_file(os.path.join(GOLD, f"unet_full_{fcase}.safetensors"))["out"]
     fl = _stats(floor["fp16" if act == "fp16" else "bf16"], full)["rel_l2"]
+    fl_unit = None
+    c1_floor = os.path.join(GOLD, f"unet_{case}_floor.safetensors")
+    if w_px != 1024 and os.path.exists(c1_floor):
+        # C1's own rounding floor per unit (tools/gen_golden_c1_floor.py: the rounded oracle on this call's inputs
+        # against the reference run), in place of the 576x1024 one
+        f1 = load_file(c1_floor)
+        torch.testing.assert_close(f1["inputs_checksum"], g["inputs_checksum"], rtol=1e-6, atol=1e-6)
+        fl_unit = f1["fp16" if act == "fp16" else "bf16"].tolist()
     tol = min(2e-2, 1.5 * fl)
     unet.acth_compute_dtype = torch.float16 if act == "fp16" else torch.bfloat16
     try:
@@ -422,8 +432,10 @@ def test_headline_window_call_matches_reference_run(dev, full_unet, act, mode, f
     assert want.shape[0] == len(branches)
     for c in range(len(branches)):
         st = _stats(got[c], want[c])
-        st["rounding_floor_rel_l2"] = fl
+        tol_c = tol if fl_unit is None else min(2e-2, 1.5 * fl_unit[c])
+        st["rounding_floor_rel_l2"] = fl if fl_unit is None else fl_unit[c]
+        st["tol"] = tol_c
         _log(f"{case}_unit{branches[c]}_{act}", st)
         assert torch.isfinite(got[c]).all()
-        assert st["rel_l2"] < tol, (c, st)
+        assert st["rel_l2"] < tol_c, (c, st)
         assert st["max_abs"] < 0.25 * st["ref_rms"], (c, st)

@@ -234,6 +234,7 @@ SIGNATURES = {
     "acth_im2col3x3": ([c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp], c_int),
     "acth_gather_rows": ([c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
     "acth_frame_mean": ([c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp], c_int),
+    "acth_gather_blocks": ([c_vp, c_int, c_vp, c_int, ctypes.c_longlong, c_vp, c_vp], c_int),
     "acth_window_input": ([c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
     "acth_cfg_euler_accum": ([c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_float, c_float, c_float, c_vp, c_vp,
                               c_int, c_int, c_vp], c_int),

@@ -13,6 +13,7 @@
 //  * acth_cfg_euler_accum    : 4-way guidance + v-prediction Euler step + window accumulate
 //                              (pipeline:731-751, EulerDiscreteScheduler.step)
 //  * acth_div_counter        : latents_all = pred_latents / counter (pipeline:755-756)
+//  * acth_gather_blocks      : batch-element row blocks copied out by index (the UNet's CFG-prefix expand)
 #include "common.h"
 
 __global__ void temb_kernel(const float* t, int n, int dim, int flip, float shift, float scale,
@@ -317,6 +318,39 @@ extern "C" int acth_div_counter(const float* acc, const float* cnt, float* out, 
   const long long n = (long long)T * S * 4;
   hipLaunchKernelGGL(div_counter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, acc, cnt,
                      out, T, S);
+  ACTH_CHECK_LAUNCH();
+  return ACTH_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// dst block i = src block idx[i] (blocks of n16 16-byte vectors): the UNet's CFG-prefix sharing copies the
+// distinct batch elements' rows out to the full batch (one launch per copy, 16-byte loads and stores; each
+// thread issues its four loads before its four stores)
+__global__ void gather_blocks_kernel(const uint4* __restrict__ src, const int* __restrict__ idx,
+                                     uint4* __restrict__ dst, long long n16) {
+  const int b = blockIdx.y;
+  const uint4* s = src + (long long)idx[b] * n16;
+  uint4* d = dst + (long long)b * n16;
+  const long long i0 = (long long)blockIdx.x * 1024 + threadIdx.x;
+  uint4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (i0 + 256 * k < n16) v[k] = s[i0 + 256 * k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (i0 + 256 * k < n16) d[i0 + 256 * k] = v[k];
+}
+
+extern "C" int acth_gather_blocks(const void* src, int n_src, const int* idx, int n, long long block_bytes,
+                                  void* dst, hipStream_t stream) {
+  if (n < 0 || n > 65535 || n_src <= 0 || block_bytes < 0 || block_bytes % 16) return ACTH_EINVAL;
+  if (n == 0 || block_bytes == 0) return ACTH_OK;   // no work: the (possibly empty) buffers are not touched
+  if (!src || !idx || !dst || ((uintptr_t)src | (uintptr_t)dst) % 16) return ACTH_EINVAL;
+  const long long n16 = block_bytes / 16;
+  const long long gx = (n16 + 1023) / 1024;
+  if (gx > 0x7fffffffLL) return ACTH_EINVAL;
+  hipLaunchKernelGGL(gather_blocks_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, stream,
+                     (const uint4*)src, idx, (uint4*)dst, n16);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -725,6 +725,25 @@ def gather_rows(src: torch.Tensor, idx: torch.Tensor, nb: int, Ls: int, dst: tor
     return dst
 
 
+def gather_blocks(src: torch.Tensor, n_src: int, idx: torch.Tensor, idx_max: int) -> torch.Tensor:
+    """``src`` viewed as ``n_src`` equal row blocks; returns the blocks ``idx`` names, in order
+    (out block i = src block idx[i]). ``idx``: device int32; ``idx_max``: the caller's host-side bound on its
+    entries (the kernel does not check them)."""
+    lib = _lib.load(act_dtype())
+    _need(idx, torch.int32, "gather_blocks idx")
+    if not src.is_contiguous() or n_src < 1 or src.shape[0] % n_src:
+        raise _lib.ActhError(f"gather_blocks: src {tuple(src.shape)} is not {n_src} contiguous row blocks")
+    if not 0 <= int(idx_max) < n_src:
+        raise _lib.ActhError(f"gather_blocks: index bound {idx_max} outside [0, {n_src})")
+    n = idx.numel()
+    per = src.shape[0] // n_src
+    out = torch.empty((n * per, *src.shape[1:]), device=src.device, dtype=src.dtype)
+    block_bytes = src.numel() // n_src * src.element_size()
+    _lib.check(lib.acth_gather_blocks(_p(src), n_src, _p(idx), n, block_bytes, _p(out), _stream()),
+               "acth_gather_blocks")
+    return out
+
+
 def frame_mean(x: torch.Tensor, B: int, F: int, T: int) -> torch.Tensor:
     """x rows ((b*F + f)*T + t) -> rows (b*T + t), mean over f."""
     lib = _lib.load(act_dtype())

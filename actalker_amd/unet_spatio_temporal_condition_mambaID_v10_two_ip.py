@@ -309,14 +309,14 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         self._batched_ctx_projections(ctx, temb_only)
         return ctx
 
-    def _dev_ints(self, values, device) -> torch.Tensor:
-        """int64 device copy of a small host list, cached by content (the sampler repeats the same
+    def _dev_ints(self, values, device, dtype=torch.int64) -> torch.Tensor:
+        """Device copy of a small host list, cached by content (the sampler repeats the same
         prefix maps every step; a pageable host -> device copy waits for the stream to drain)."""
         cache = self.__dict__.setdefault("_acth_ints", {})
-        key = (tuple(values), str(device))
+        key = (tuple(values), str(device), dtype)
         t = cache.get(key)
         if t is None:
-            t = cache[key] = torch.tensor(values, dtype=torch.int64, device=device)
+            t = cache[key] = torch.tensor(values, dtype=dtype, device=device)
         return t
 
     def _batched_ctx_projections(self, ctx, temb_only: bool = False):
@@ -470,14 +470,17 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             Bu = len(uniq)
             pos = {b: i for i, b in enumerate(uniq)}
             ui = self._dev_ints(uniq, x_tok.device)
-            inv = self._dev_ints([pos[prefix_src[b]] for b in range(B)], x_tok.device)
+            ui32 = self._dev_ints(uniq, x_tok.device, torch.int32)
+            inv_h = [pos[prefix_src[b]] for b in range(B)]
+            inv = self._dev_ints(inv_h, x_tok.device, torch.int32)
 
             def take(t, per):                # rows of the distinct elements (t holds B x per rows)
+                if t.is_cuda and t.is_contiguous() and (t.numel() // B * t.element_size()) % 16 == 0:
+                    return ops.gather_blocks(t, B, ui32, max(uniq))
                 return t.reshape(B, per, *t.shape[1:]).index_select(0, ui).reshape(Bu * per, *t.shape[1:])
 
-            def expand(t):                   # distinct-element rows -> the full batch
-                per = t.shape[0] // Bu
-                return t.reshape(Bu, per, *t.shape[1:]).index_select(0, inv).reshape(B * per, *t.shape[1:])
+            def expand(t):                   # distinct-element rows -> the full batch (one block-gather launch)
+                return ops.gather_blocks(t.contiguous(), Bu, inv, max(inv_h))
 
             if isinstance(encoder_hidden_states, tuple):
                 ehs_u = (take(encoder_hidden_states[0], F), [take(e, F) for e in encoder_hidden_states[1]])

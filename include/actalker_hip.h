@@ -19,10 +19,11 @@
  *   - stream-ordered on `stream`; no allocation, no host synchronisation (graph-capturable);
  *   - return ACTH_OK (0), ACTH_EINVAL (-1) for a rejected shape/alignment, or ACTH_ELAUNCH (-2)
  *     when the launch failed;
- *   - a call with no work (zero rows / an empty batch: M, B, nbatch, nb, Sq = 0, as torch ops accept empty
+ *   - a call with no work (zero rows / an empty batch: M, B, nbatch, nb, Sq, n = 0, as torch ops accept empty
  *     tensors) returns ACTH_OK without launching and reads no pointer (an empty tensor's data pointer may
- *     be NULL). A negative value of that primary size stays ACTH_EINVAL; the attention entry points also
- *     check their other sizes (>= 0, F in 1..32) before the no-work return, the others do not inspect
+ *     be NULL). A negative value of that primary size stays ACTH_EINVAL; the attention entry points and
+ *     acth_gather_blocks also check their other sizes (>= 0, F in 1..32, block_bytes % 16) before the
+ *     no-work return, the others do not inspect
  *     the remaining fields of a call with no work.
  */
 #ifndef ACTALKER_HIP_H
@@ -278,6 +279,12 @@ int acth_gather_rows(const void* src, int lds, int Ls, const int* idx, int n, vo
                      int nb, int C, hipStream_t stream);
 int acth_frame_mean(const void* x, int ldx, int B, int F, int T, int C, void* out, int ldo,
                     hipStream_t stream);
+/* dst block i = src block idx[i], i < n (block_bytes each, a multiple of 16; src, dst 16-byte aligned; idx on the
+ * device, entries in [0, n_src) -- not checked on the device; n <= 65535). The UNet's CFG-prefix sharing
+ * (actalker_amd UNet.forward_tokens) copies the distinct batch elements' activations out to the full batch with it,
+ * where the reference simply runs every CFG branch through the whole UNet (pipeline:712-729). */
+int acth_gather_blocks(const void* src, int n_src, const int* idx, int n, long long block_bytes, void* dst,
+                       hipStream_t stream);
 
 /* ---- sampler loop (pipeline_svd_audio_adapter_motionexp_idembed_vasa_two_ip.py:684-756) */
 int acth_window_input(const float* lat, const int* frame_idx, const float* img, const int* branch,

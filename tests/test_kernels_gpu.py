@@ -868,6 +868,22 @@ def test_layout_and_gather(dev):
     assert rel(fm, refm) < 5e-3
 
 
+@pytest.mark.parametrize("n_src,per,C,idx", [(2, 9216 * 3, 320, [0, 1, 1]), (4, 37, 8, [0, 1, 1, 3, 3, 1]),
+                                             (3, 1, 8, [2, 0]), (1, 1033, 640, [0, 0, 0, 0]), (2, 5, 8, [])])
+def test_gather_blocks_matches_index_select(dev, n_src, per, C, idx):
+    """acth_gather_blocks (the UNet's CFG-prefix expand) is bitwise index_select over the batch blocks: repeated
+    indices, one-row blocks, a block count that is not a multiple of the 1024-vector launch chunk, no indices."""
+    src = bf(rnd(n_src * per, C)).to(dev)
+    ix = torch.tensor(idx, dtype=torch.int32, device=dev)
+    got = ops.gather_blocks(src, n_src, ix, max(idx) if idx else 0)
+    want = src.view(n_src, per, C).index_select(0, ix.long()).reshape(-1, C)
+    assert got.shape == want.shape and torch.equal(got, want)
+    with pytest.raises(Exception):
+        ops.gather_blocks(src, n_src, ix, n_src)             # host bound outside the source blocks
+    with pytest.raises(Exception):
+        ops.gather_blocks(src[:, :C - 1], n_src, ix, 0)      # rows not contiguous
+
+
 def test_cfg_euler_accum(dev):
     F_, S, T = 3, 10, 6
     noise = rnd(4 * F_ * S, 4)

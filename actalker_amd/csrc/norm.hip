@@ -312,9 +312,11 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const ActhGroupNormDesc p
     double a1 = 0.0, a2 = 0.0;
     for (int r = 0; r < rows_par; ++r)
       for (int c = t * cpg; c < (t + 1) * cpg; ++c) { a1 += red[r * 2 * p.C + c]; a2 += red[r * 2 * p.C + p.C + c]; }
-    double* acc = p.ws + ((size_t)stat * p.G + t) * 2;
-    atomicAdd(acc, a1);
-    atomicAdd(acc + 1, a2);
+    // this block's partial sums in its own slot (no atomics, no zeroed workspace): gn_apply_kernel adds a
+    // statistics batch's slots in block order, so the statistics are bitwise reproducible run to run
+    double* part = p.ws + (((size_t)stat * gridDim.x + blockIdx.x) * p.G + t) * 2;
+    part[0] = a1;
+    part[1] = a2;
   }
 }
 
@@ -341,7 +343,7 @@ __device__ __forceinline__ void gn_finish(const ActhGroupNormDesc& p, long long 
 
 #define GN_MAX_GROUPS 1024
 // grid: M / rows_per_blk blocks; every block's rows lie in one statistics batch
-__global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p, int rows_per_blk) {
+__global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p, int rows_per_blk, int nblk) {
   const int nch = p.C >> 3;
   const int nchl = nch < 256 ? nch : 256;
   const int rows_par = 256 / nchl;
@@ -354,12 +356,41 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p
   // thread: the per-channel form spent more issue on fp64 divides and square roots than the
   // block's 128 rows of streaming)
   __shared__ float s_mean[GN_MAX_GROUPS], s_rstd[GN_MAX_GROUPS];
+  __shared__ double s_a[2][256];
   {
     const double n = (double)cpg * p.rows_per_stat;
+    // the nblk stats blocks' partial sums of this batch: lane j of group g adds slots j, j + lanes, ... (at
+    // most a few independent loads per thread), then the lanes are folded in lane order -- a fixed order
+    const double* part = p.ws + (size_t)stat * nblk * p.G * 2;
+    const int lanes = p.G <= 256 ? 256 / p.G : 1;
+    if (lanes > 1) {
+      const int g = t % p.G, j = t / p.G;
+      double a1 = 0.0, a2 = 0.0;
+      if (j < lanes)
+        for (int k = j; k < nblk; k += lanes) {
+          const double* q = part + ((size_t)k * p.G + g) * 2;
+          a1 += q[0];
+          a2 += q[1];
+        }
+      s_a[0][t] = a1;
+      s_a[1][t] = a2;
+      __syncthreads();
+    }
     for (int g = t; g < p.G; g += 256) {
-      const double* acc = p.ws + ((size_t)stat * p.G + g) * 2;
-      const double mean = acc[0] / n;
-      double var = acc[1] / n - mean * mean;
+      double a1 = 0.0, a2 = 0.0;
+      if (lanes > 1) {
+        for (int j = 0; j < lanes; ++j) {
+          a1 += s_a[0][j * p.G + g];
+          a2 += s_a[1][j * p.G + g];
+        }
+      } else {
+        for (int k = 0; k < nblk; ++k) {
+          a1 += part[((size_t)k * p.G + g) * 2];
+          a2 += part[((size_t)k * p.G + g) * 2 + 1];
+        }
+      }
+      const double mean = a1 / n;
+      double var = a2 / n - mean * mean;
       if (var < 0.0) var = 0.0;
       s_mean[g] = (float)mean;
       s_rstd[g] = (float)(1.0 / sqrt(var + (double)p.eps));
@@ -404,10 +435,35 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const ActhGroupNormDesc p
   }
 }
 
+// Row span per statistics block: as many blocks as the chip holds at once (its 32 KB of LDS allow 5 per
+// CU), split evenly over the statistics batches, so the pass is one full round of blocks (the former
+// power-of-two spans gave 1512 blocks against 1280 slots at every UNet level: a second, 18 % round).
+// *nblk: stats blocks per batch (each owns a G x 2 fp64 partial-sum slot of the workspace).
+static void gn_split(long long nstat, int rows_per_stat, int* gs_rows, int* nblk) {
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gn_stats_kernel, 256, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 4;
+    slots = ncu * per_cu;
+  }
+  const long long per_stat = nstat >= slots ? 1 : slots / nstat;
+  int g = (int)((rows_per_stat + per_stat - 1) / per_stat);
+  if (g < 64) g = 64;
+  *gs_rows = g;
+  *nblk = (rows_per_stat + g - 1) / g;
+}
+
 extern "C" size_t acth_groupnorm_workspace_size(int M, int C, int G, int rows_per_stat) {
-  if (rows_per_stat <= 0) return 0;
-  const size_t nstat = (size_t)M / rows_per_stat;
-  return nstat * G * 2 * sizeof(double);
+  if (rows_per_stat <= 0 || M <= 0 || G <= 0) return 0;
+  const long long nstat = M / rows_per_stat;
+  if (nstat == 0) return 0;
+  int gs_rows = 0, nblk = 0;
+  gn_split(nstat, rows_per_stat, &gs_rows, &nblk);
+  return (size_t)nstat * nblk * G * 2 * sizeof(double);
 }
 
 extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
@@ -422,25 +478,11 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   const int nstat = d->M / d->rows_per_stat;
   if (nstat == 0) return ACTH_OK;
   if (nstat > 65535) return ACTH_EINVAL;
-  if (hipMemsetAsync(d->ws, 0, (size_t)nstat * d->G * 2 * sizeof(double), stream) != hipSuccess)
-    return ACTH_ELAUNCH;
-  // Row span per statistics block: as many blocks as the chip holds at once (its 32 KB of LDS allow 5 per
-  // CU), split evenly over the statistics batches, so the pass is one full round of blocks (the former
-  // power-of-two spans gave 1512 blocks against 1280 slots at every UNet level: a second, 18 % round).
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, ncu = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || ncu <= 0)
-      ncu = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gn_stats_kernel, 256, 0) != hipSuccess || per_cu <= 0)
-      per_cu = 4;
-    slots = ncu * per_cu;
-  }
-  const long long per_stat = nstat >= slots ? 1 : slots / nstat;
-  int gs_rows = (int)((d->rows_per_stat + per_stat - 1) / per_stat);
-  if (gs_rows < 64) gs_rows = 64;
-  dim3 g1((d->rows_per_stat + gs_rows - 1) / gs_rows, nstat);
+  // the workspace (acth_groupnorm_workspace_size bytes) needs no clearing: every slot is written by the stats
+  // pass before the apply pass reads it
+  int gs_rows = 0, nblk = 0;
+  gn_split(nstat, d->rows_per_stat, &gs_rows, &nblk);
+  dim3 g1(nblk, nstat);
   hipLaunchKernelGGL(gn_stats_kernel, g1, dim3(256), 0, stream, *d, gs_rows);
   ACTH_CHECK_LAUNCH();
   int rpb = 128;
@@ -448,7 +490,7 @@ extern "C" int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream) {
   // fewer rows per block while the grid would not fill the chip twice over (2048 = 8 resident blocks on
   // each of 256 CUs): the level-1 / level-2 shapes had 1512 / 378 blocks of 128 rows
   while (rpb > 32 && (d->M / rpb) < 4096 && d->rows_per_stat % (rpb >> 1) == 0) rpb >>= 1;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)(d->M / rpb)), dim3(256), 0, stream, *d, rpb);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3((unsigned)(d->M / rpb)), dim3(256), 0, stream, *d, rpb, nblk);
   ACTH_CHECK_LAUNCH();
   return ACTH_OK;
 }

@@ -197,6 +197,8 @@ typedef struct ActhGroupNormDesc {
   const void* res; int ldres;
 } ActhGroupNormDesc;
 int acth_groupnorm(const ActhGroupNormDesc* d, hipStream_t stream);
+/* ws: acth_groupnorm_workspace_size bytes, no clearing needed (each statistics block writes its own fp64
+ * partial-sum slot; the apply pass adds them in a fixed order, so the output is bitwise reproducible) */
 size_t acth_groupnorm_workspace_size(int M, int C, int G, int rows_per_stat);
 
 /* ---- SS2D_cond_v10 scatter-back + sum + out_norm (mamba_layer.py:1963-1985) */

@@ -221,6 +221,41 @@ def test_batched_ctx_projections_match_per_module(dev, tiny):
     assert rel(batched, single) < 1e-3
 
 
+def test_ctx_token_cache_reuses_and_invalidates(dev, tiny):
+    """The per-call token side of the UNet context (ID / audio / VASA rows, frame means, their batched projections)
+    is reused for the same prompt tensors and packed weights, and recomputed -- to the same values -- after an
+    in-place write to a prompt tensor or a weight update."""
+    from actalker_amd import ops
+    unet, sd, cfg = tiny
+    sample, t, ehs, added, pose, masks = ge._tiny_inputs(B=3, F=3, H=16, W=32, seed=13)
+    B, F = 3, 3
+    e = (ehs[0].to(dev), [a.to(dev) for a in ehs[1]])
+    cak = {"ip_adapter_masks": masks}
+    unet.__dict__.pop("_acth_tok_cache", None)
+    attn = unet._ctx_mods()[1][0]                    # first spatial attn2 (its to_v(ID token) is batched)
+    w = attn.to_v.weight
+    w_old = w.detach().clone()
+    try:
+        with torch.no_grad(), ops.compute_dtype(unet.compute_dtype()):
+            c1 = unet._prep_ctx(B, F, t.to(dev), e, added.to(dev), cak)
+            c2 = unet._prep_ctx(B, F, t.to(dev), e, added.to(dev), cak)
+            assert c2.vid is c1.vid and c2.id_tok is c1.id_tok and c2.ipkv is c1.ipkv      # hit
+            assert c2.tproj is not c1.tproj                                                 # temb: every call
+            e[1][0].mul_(1.0)                        # same values, new version: recomputed
+            c3 = unet._prep_ctx(B, F, t.to(dev), e, added.to(dev), cak)
+            assert c3.vid is not c1.vid
+            for k in c1.ipkv:
+                assert torch.equal(c3.ipkv[k], c1.ipkv[k])
+            w.mul_(2.0)                              # a weight update: new packed weights, new projections
+            c4 = unet._prep_ctx(B, F, t.to(dev), e, added.to(dev), cak)
+            assert c4.vid is not c3.vid
+            assert not torch.equal(c4.vid[id(attn)], c3.vid[id(attn)])
+    finally:
+        with torch.no_grad():
+            w.copy_(w_old)
+    assert len(unet.__dict__["_acth_tok_cache"]) <= unet._ACTH_TOK_CACHE
+
+
 def test_paired_mamba_scan_matches_per_branch(dev, tiny):
     """SS2D_cond_v10 with both branches' scans in one acth_selective_scan2 launch == one launch per branch,
     bit for bit (the tiny inputs' masks select part of each frame, so both branches scan)."""

@@ -111,6 +111,13 @@ def test_zero_work_calls_are_noops(which):
         assert fn(ctypes.byref(d), None) == -1, (fn.__name__, size)
     s0, s1 = _lib.ScanDesc(), _lib.ScanDesc()
     assert lib.acth_selective_scan2(ctypes.byref(s0), ctypes.byref(s1), None) == 0
+    # block gather: no blocks (or empty blocks) is a no-op on NULL pointers; bad sizes are rejected first
+    assert lib.acth_gather_blocks(None, 2, None, 0, 64, None, None) == 0
+    assert lib.acth_gather_blocks(None, 2, None, 3, 0, None, None) == 0
+    assert lib.acth_gather_blocks(None, 2, None, -1, 64, None, None) == -1
+    assert lib.acth_gather_blocks(None, 2, None, 0, 24, None, None) == -1       # block_bytes % 16
+    assert lib.acth_gather_blocks(None, 0, None, 0, 64, None, None) == -1       # no source blocks
+    assert lib.acth_gather_blocks(None, 2, None, 3, 64, None, None) == -1       # work with NULL pointers
 
 
 def test_no_cpu_fallback():

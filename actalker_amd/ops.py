@@ -72,6 +72,8 @@ def _rows(t: torch.Tensor, what: str) -> int:
 # ACTH_GEMM_TILE_FLAGS: main-loop flag bits OR-ed into every GEMM's tile word (0x1000 ring, 0x2000 4-phase loop):
 # A/B of whole-step timings on one box (tools/ab_gemm.py does the same per shape)
 _GEMM_TILE_FLAGS = int(os.environ.get("ACTH_GEMM_TILE_FLAGS", "0"), 0) & 0x3000
+# ACTH_GEMM_RING_K: dense products with K >= this also take the ring main loop (0: the convs only, the default)
+_GEMM_RING_K = int(os.environ.get("ACTH_GEMM_RING_K", "0"))
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optional[torch.Tensor] = None,
@@ -199,7 +201,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, M: Optional[int] = None, a2: Optio
         if out.shape[0] <= last or out.shape[1] < n_out:
             raise _lib.ActhError(f"gemm: out {tuple(out.shape)} too small for orow {tuple(orow)} at M={M}")
         d.orow_div, d.orow_stride, d.orow_off = od, ost, oo
-    d.tile = tile | _GEMM_TILE_FLAGS
+    flags = _GEMM_TILE_FLAGS
+    if _GEMM_RING_K and not flags and d.amode == 0 and K >= _GEMM_RING_K:
+        flags = 0x1000
+    d.tile = tile | flags
     _lib.check(lib.acth_gemm(ctypes.byref(d), _stream()), "acth_gemm")
     return out
 

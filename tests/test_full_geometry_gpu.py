@@ -269,12 +269,21 @@ def test_c1_loop_matches_cpu_oracle(dev, full_unet, act):
         unet.acth_compute_dtype = None
     want = g["latents"]
     st = _stats(got, want)
-    # fp16: no fp16-rounded C1 loop exists (~8 h of CPU); the cap sits ~2x above the measured 2.2e-3
-    # (profiles/r4_step6_window_twins_parity.jsonl), ~10x tighter than the bf16 cap
+    # No rounded C1 *loop* exists (the fp32 oracle loop alone took 19 671 s; a rounded one ~11 CPU-hours). The loop
+    # is held to 1.5x the rounding floor of one C1 window call instead (tests/golden/unet_c1win14_mode0_floor:
+    # the oracle under bf16 / fp16 rounding against the reference run, largest unit): the 25-step loop's own
+    # deviation measured at that call floor's size (bf16 1.72e-2 vs 1.72-1.80e-2, fp16 2.20e-3 vs 2.21-2.25e-3,
+    # profiles/r4_step6_window_twins_parity.jsonl, r6_c1_floor.log), capped at the former fixed bounds.
     tol = 5e-3 if act == "fp16" else 5e-2
+    fpath = os.path.join(GOLD, "unet_c1win14_mode0_floor.safetensors")
+    if os.path.exists(fpath):
+        fl = load_file(fpath)["fp16" if act == "fp16" else "bf16"]
+        st["c1_call_floor_rel_l2"] = float(fl.max())
+        tol = min(tol, 1.5 * st["c1_call_floor_rel_l2"])
     if "latents_bf16" in g and act == "bf16":
         st["bf16_rounding_rel_l2"] = ((g["latents_bf16"] - want).norm() / want.norm()).item()
         tol = min(tol, 1.5 * st["bf16_rounding_rel_l2"])
+    st["tol"] = tol
     _log(f"c1_loop25_mode0_{act}", st)
     assert torch.isfinite(got).all()
     assert st["rel_l2"] < tol, st

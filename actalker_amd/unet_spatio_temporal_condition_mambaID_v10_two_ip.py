@@ -304,7 +304,11 @@ class UNetSpatioTemporalConditionModel(nn.Module):
         key = (B, F, str(ops.act_dtype()), ctx.audio_zero, ctx.vasa_zero, temb_only, batch)
         cache = self.__dict__.setdefault("_acth_tok_cache", [])
         hit = None
-        if not temb_only:
+        # only on the device's default stream: an entry made on one stream and read (or freed) on another would need
+        # cross-stream events (LoopConfig.concurrent_calls > 1 runs calls on side streams)
+        use_cache = (not temb_only and dev.type == "cuda"
+                     and torch.cuda.current_stream(dev) == torch.cuda.default_stream(dev))
+        if use_cache:
             for i, ent in enumerate(cache):
                 if (ent["key"] == key and len(ent["srcs"]) == len(srcs)
                         and all(a is b and a._version == vb for a, b, vb in zip(srcs, ent["srcs"], ent["ver"]))
@@ -328,7 +332,7 @@ class UNetSpatioTemporalConditionModel(nn.Module):
             ctx.vasa_mean = ops.frame_mean(ctx.vasa_tok, B, F, 1)
         ctx.id_mean = ops.frame_mean(ctx.id_tok, B, F, 1)
         self._run_ctx_token_jobs(ctx, jobs)
-        if not temb_only:
+        if use_cache:
             names = ("id_tok", "audio_tok", "vasa_tok", "n_audio", "id_mean", "audio_mean", "vasa_mean", "vid",
                      "ipkv", "ipvb", "mamba_proj")
             cache.insert(0, dict(key=key, srcs=srcs, ver=tuple(t._version for t in srcs),
